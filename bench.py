@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric on MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+
+Headline (`value`): UTS nodes/sec over the whole job for the BASELINE
+multi-GPU config, test/uts T3L (-t 0 -b 2000 -q 0.200014 -m 5 -r 7,
+111,345,631 nodes). One step = one complete search of the tree: every rank
+expands the top `split` levels identically and then searches the T3L nodes
+it owns at depth `split` (hash of the node state mod N) on its own GPU with
+the persistent work-stealing megakernel; per-step totals are combined with an
+RCCL all-reduce (sum nodes/leaves, max depth) and checked bit-exact against
+the published tree statistics every step. Scaling is STRONG (the tree is
+fixed as N grows); T3L is span-bound (17,844 dependent SHA-1 levels).
+
+At N=1 the same JSON line also carries the other BASELINE configs measured
+in the same process (T1 nodes/s, forasync triad HBM GB/s with its roofline,
+fib(30) tasks/s, Smith-Waterman 64K cells/s) and the host-CPU baseline: the
+repo's C restatement of HClib's work-stealing runtime (oracle/, "port") on
+T3L with the box's CPU share.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+T3L = "-t 0 -b 2000 -q 0.200014 -m 5 -r 7"
+T3L_GOLD = (111345631, 89076904, 17844)  # test/uts/sample_trees.sh:42-43
+T1 = "-t 1 -a 3 -d 10 -b 4 -r 19"
+T1_GOLD = (4130071, 3305118, 10)          # test/uts/sample_trees.sh:17-18
+HBM_PEAK_GBS = 8000.0                      # MI355X_MICROARCH.md chip table (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup_dist(n_gpus):
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def barrier(world):
+    import torch
+
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def allreduce_counts(world, nodes, leaves, depth):
+    import torch
+
+    if world == 1:
+        return nodes, leaves, depth
+    import torch.distributed as dist
+
+    t = torch.tensor([nodes, leaves], dtype=torch.int64, device="cuda")
+    d = torch.tensor([depth], dtype=torch.int64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    return int(t[0]), int(t[1]), int(d[0])
+
+
+def max_over_ranks(world, x):
+    import torch
+
+    if world == 1:
+        return x
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def uts_step(H, rank, world, split):
+    r = H.uts(T3L, rank, world, split) if world > 1 else H.uts(T3L)
+    return r
+
+
+def measure_triad(H, reps=20):
+    """forasync triad (BASELINE config 1): 2^28 fp32, a = b + 3*c; HIP events
+    on the stream the kernel is launched on; checked bit-exact."""
+    import torch
+
+    n = 1 << 28
+    g = torch.Generator(device="cuda").manual_seed(1)
+    b = torch.rand(n, device="cuda", generator=g)
+    c = torch.rand(n, device="cuda", generator=g)
+    a = torch.empty(n, device="cuda")
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        H.triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), 3.0, n, st.cuda_stream)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        H.triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), 3.0, n, st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    ok = bool(torch.equal(a, torch.add(b, torch.mul(c, 3.0))))
+    del a, b, c
+    torch.cuda.empty_cache()
+    algo = 12 * n  # read b, c; write a (write-allocate not counted)
+    return {"ms": ms, "gbs": algo / ms / 1e6, "bytes": algo, "bit_exact": ok}
+
+
+def load_pmc_traffic():
+    """HBM bytes per triad launch from the committed rocprofv3 PMC summary
+    (profiles/), corrected per MI355X_MICROARCH.md (FETCH_SIZE x2 on gfx950)."""
+    p = os.path.join(ROOT, "profiles", "triad_pmc.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p)).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def cpu_baseline(threads):
+    """Host-CPU HClib (oracle/ C restatement, "port") on T3L; bounded sample:
+    one full T3L search (~2-4 s at 16 threads)."""
+    import ctypes as C
+
+    from oracle import loader as L
+
+    lib = L.cpu_runtime()
+    p = L.parse_uts_args(T3L)
+    n, lv, d, sec = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
+    assert lib.ohc_uts(threads, C.byref(p), C.byref(n), C.byref(lv), C.byref(d), C.byref(sec)) == 0
+    assert (n.value, lv.value, d.value) == T3L_GOLD, "CPU baseline miscounted"
+    return {"value": n.value / sec.value, "unit": "nodes/s", "cores": threads, "kind": "port",
+            "sample": "one full UTS T3L search (111,345,631 nodes) on oracle/hclib_cpu.c, "
+                      f"{threads} worker threads, {sec.value:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--split", type=int, default=64, help="replicated top levels before sharding")
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    import torch  # noqa: F401  (one HIP runtime for torch + the module)
+
+    rank, world, local = setup_dist(args.gpus)
+    import hclib_amd as H
+
+    H.init(local)
+
+    for _ in range(args.warmup):
+        r = uts_step(H, rank, world, args.split)
+    barrier(world)
+    t0 = time.perf_counter()
+    kernel_ms = []
+    last = None
+    for _ in range(args.steps):
+        r = uts_step(H, rank, world, args.split)
+        kernel_ms.append(r["kernel_ms"])
+        last = r
+    barrier(world)
+    elapsed = max_over_ranks(world, time.perf_counter() - t0)
+    tot = allreduce_counts(world, last["nodes"], last["leaves"], last["max_depth"])
+    if tot != T3L_GOLD:
+        raise SystemExit(f"T3L mismatch: {tot} != {T3L_GOLD}")
+    value = T3L_GOLD[0] * args.steps / elapsed
+    if rank != 0:
+        return
+
+    out = {
+        "metric": "UTS nodes/sec (tasks/sec) at 1/2/4/8 MI355X vs host-CPU HClib; forasync HBM GB/s",
+        "value": value,
+        "unit": "nodes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (UTS trees are generated from their published parameters; no dataset)",
+        "config": {
+            "workload": f"test/uts T3L ({T3L}) sharded over {world} GPU(s), split depth {args.split}",
+            "nodes": T3L_GOLD[0],
+            "bit_exact": True,
+            "uts_kernel_ms_rank0": sum(kernel_ms) / len(kernel_ms),
+            "parallelism": f"shard{world} (hash-partitioned frontier, RCCL all-reduce of counts)",
+        },
+    }
+    if world == 1 and not args.no_extras:
+        tri = measure_triad(H)
+        traffic = load_pmc_traffic()
+        out["roofline"] = {
+            "bound": "hbm",
+            "kernel": "k_triad_f32 (hclib_forasync 1-D triad, BASELINE config 1)",
+            "achieved": tri["gbs"],
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": tri["gbs"] / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": tri["bytes"],
+            "avg_launch_ms": tri["ms"],
+            "bit_exact": tri["bit_exact"],
+        }
+        # UTS kernel bound: span (critical path of dependent SHA-1s)
+        uts_ms = out["config"]["uts_kernel_ms_rank0"]
+        out["uts_span"] = {
+            "bound": "span", "levels": T3L_GOLD[2],
+            "ns_per_level": uts_ms * 1e6 / T3L_GOLD[2],
+        }
+        t1 = min((H.uts(T1) for _ in range(3)), key=lambda r: r["kernel_ms"])
+        assert (t1["nodes"], t1["leaves"], t1["max_depth"]) == T1_GOLD
+        fv, fst = H.fib(30)
+        assert fv == 832040
+        s1 = H.sw_map(open(os.path.join(ROOT, "tests/golden/sw/string1-huge.txt"), "rb").read())[:65536]
+        s2 = H.sw_map(open(os.path.join(ROOT, "tests/golden/sw/string2-huge.txt"), "rb").read())[:65536]
+        score, swst = H.sw(s1, s2, 256, 256)
+        assert score == 128772
+        out["configs"] = {
+            "uts_t1_1gpu": {"nodes_per_s": T1_GOLD[0] / (t1["kernel_ms"] * 1e-3),
+                            "kernel_ms": t1["kernel_ms"]},
+            "forasync_triad_2p28": {"GB_per_s": tri["gbs"], "ms": tri["ms"]},
+            "fib30_gpu": {"tasks_per_s": fst["tasks"] / (fst["kernel_ms"] * 1e-3),
+                          "tasks": fst["tasks"], "kernel_ms": fst["kernel_ms"]},
+            "sw_64k": {"cells_per_s": swst["cells_per_s"], "kernel_ms": swst["kernel_ms"],
+                       "score": score},
+        }
+        threads = int(os.environ.get("HCLIB_BENCH_CPU_THREADS",
+                                     os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))))
+        threads = max(1, min(threads, 16, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(threads)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

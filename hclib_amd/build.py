@@ -1,0 +1,91 @@
+"""Build the MI355X module library in-tree with hipcc (gfx950 only).
+
+    python -m hclib_amd.build        -> hclib_amd/lib/libhclib_amd.so
+
+The library holds every hand-written HIP kernel plus the C ABI of
+include/hclib_hip.h (modules/hip) and include/hclib.h (the HClib C API).
+Sources compile in parallel; an unchanged source is not rebuilt.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OUT = os.path.join(PKG, "lib")
+LIB = os.path.join(OUT, "libhclib_amd.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+SOURCES = ["module.hip", "forasync.hip", "uts.hip", "fib.hip", "sw.hip", "hclib_api.hip"]
+CFLAGS = [
+    f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+    "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result",
+    "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
+]
+
+
+def _hash(paths):
+    h = hashlib.sha1()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(CFLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def _headers():
+    hs = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith(".h")]
+    inc = os.path.join(ROOT, "include")
+    hs += [os.path.join(inc, f) for f in sorted(os.listdir(inc)) if f.endswith(".h")]
+    return hs
+
+
+def _compile(src: str, hdrs) -> str:
+    path = os.path.join(CSRC, src)
+    obj = os.path.join(OUT, src.replace(".hip", "") + "." + _hash([path] + hdrs) + ".o")
+    if not os.path.exists(obj):
+        cmd = [HIPCC] + CFLAGS + ["-c", "-x", "hip", path, "-o", obj + ".tmp"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+        os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build(verbose: bool = True) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    hdrs = _headers()
+    srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdrs), srcs))
+    stamp = os.path.join(OUT, ".stamp")
+    key = "|".join(objs)
+    if not os.path.exists(LIB) or not os.path.exists(stamp) or open(stamp).read() != key:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs + [
+            "-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+        os.replace(LIB + ".tmp", LIB)
+        with open(stamp, "w") as f:
+            f.write(key)
+    # drop stale objects
+    keep = set(objs)
+    for f in os.listdir(OUT):
+        p = os.path.join(OUT, f)
+        if f.endswith(".o") and p not in keep:
+            os.remove(p)
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build()
+    sys.exit(0)

@@ -1,0 +1,184 @@
+// fib.hip — the fib workload (test/fib/fib.c) as a device task kind.
+//
+// Each fib(n) call is one task (one lane-item), exactly as each
+// hclib_async(fib, ...) is one task in the reference (fib.c:57-71). A task
+// with n >= 2 opens a finish scope: a join record whose counter starts at 2
+// (the two child asyncs; the reference's finish counter is the owner's 1 +
+// the two check-ins, src/hclib-runtime.c:1219-1247, 431-446). Children add
+// their result and check out with ONE 64-bit atomic: word = count<<56 | sum.
+// The child that brings the count to zero runs the continuation
+// (res = lhs + rhs, fib.c:70) inline and checks out of the parent scope —
+// the GPU analogue of help_finish's work-shift (no stacks, no fibers). This
+// also is the DDT form (fib.c:113-141): the join word is the promise pair
+// subres[0..1] and the last put releases fib_ddt_res.
+#include <string.h>
+
+#include "hx_module.h"
+
+namespace hx {
+
+constexpr uint32_t kFibRoot = 0xffffffffu;
+constexpr unsigned long long kOne = 1ull << 56;
+constexpr unsigned long long kSumMask = kOne - 1;
+
+struct alignas(16) FibJoin {
+    unsigned long long word;  // count << 56 | partial sum
+    uint32_t parent;          // join index of the enclosing scope, or kFibRoot
+    uint32_t pad;
+};
+
+struct FibCtx {
+    int n;
+    FibJoin *joins;
+    uint32_t *join_next;  // bump allocator (one atomic per wave batch)
+    uint32_t join_cap;
+    unsigned long long *result;
+};
+
+struct FibKind {
+    static constexpr int kWords = 4;  // n, join, (unused), start
+    static constexpr int kMaxOut = 2;
+    using Ctx = FibCtx;
+    struct Acc {
+        unsigned long long tasks = 0, joins = 0;
+        __device__ void flush(SchedGlobals *g) {
+            unsigned long long t = wave_sum(tasks), j = wave_sum(joins);
+            if (lane_id() == 0) {
+                add_agent(&g->counters[0], t);
+                add_agent(&g->counters[1], j);
+            }
+        }
+    };
+    __device__ static uint32_t count(const uint32_t *) { return 1; }
+
+    __device__ static int roots(const Ctx &c, Acc &, uint32_t (*out)[kWords]) {
+        out[0][0] = (uint32_t)c.n;
+        out[0][1] = kFibRoot;
+        out[0][2] = 0;
+        out[0][3] = 0;
+        return 1;
+    }
+
+    // check out of scope j with value v; run continuations while last
+    __device__ static void check_out(const Ctx &c, Acc &acc, uint32_t j, unsigned long long v) {
+        while (j != kFibRoot) {
+            FibJoin *J = &c.joins[j];
+            const unsigned long long old = add_agent(&J->word, v - kOne);
+            if ((old >> 56) != 1) return;  // sibling still running
+            v += old & kSumMask;           // res = lhs + rhs (fib.c:70)
+            acc.joins += 1;
+            j = ld_agent(&J->parent);
+        }
+        st_agent(c.result, v);
+    }
+
+    __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *e, uint32_t,
+                                  uint32_t (*out)[kWords], uint32_t *err) {
+        acc.tasks += 1;
+        const int n = (int)e[0];
+        const bool spawn = n >= 2;
+        // one bump allocation per wave for every lane that opens a scope
+        const unsigned long long m = __ballot(spawn);
+        uint32_t base = 0;
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            if (lane_id() == leader) base = add_agent(c.join_next, (uint32_t)__popcll(m));
+            base = __shfl(base, leader, 64);
+        }
+        if (!spawn) {
+            check_out(c, acc, e[1], (unsigned long long)n);
+            return 0;
+        }
+        const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
+        if (j >= c.join_cap) {
+            dev_error(err, kErrArena);
+            return 0;
+        }
+        FibJoin *J = &c.joins[j];
+        st_agent(&J->word, 2ull << 56);
+        st_agent(&J->parent, e[1]);
+        out[0][0] = (uint32_t)(n - 1);
+        out[0][1] = j;
+        out[0][2] = 0;
+        out[0][3] = 0;
+        out[1][0] = (uint32_t)(n - 2);
+        out[1][1] = j;
+        out[1][2] = 0;
+        out[1][3] = 0;
+        return 2;
+    }
+};
+
+constexpr int kFibCap = 512;
+
+__global__ __launch_bounds__(64) void k_fib(FibCtx ctx, PoolView pool, SchedGlobals *g,
+                                            SchedConfig cfg) {
+    __shared__ WaveStack<FibKind, kFibCap> st;
+    run_worker<FibKind, kFibCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
+}
+
+}  // namespace hx
+
+using namespace hx;
+
+extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *result) {
+    if (n < 0 || n > 80 || !value) {
+        set_error("hclib_hip_fib: n must be in [0, 80]");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    Module &m = mod();
+    // scopes = internal nodes of the call tree = fib(n+1) - 1
+    unsigned long long a = 0, b = 1;
+    for (int i = 0; i <= n; ++i) {
+        unsigned long long t = a + b;
+        a = b;
+        b = t;
+    }
+    const unsigned long long scopes = a;  // fib(n+1)
+    if (scopes > 0xfffffff0ull) {
+        set_error("hclib_hip_fib: n too large for the join arena");
+        return HCLIB_HIP_EINVAL;
+    }
+    const size_t jb = sizeof(FibJoin) * (size_t)(scopes + 1);
+    void *dmem = nullptr;
+    HX_HIP(hipMalloc(&dmem, jb + 512));
+    FibCtx ctx;
+    ctx.n = n;
+    ctx.joins = (FibJoin *)dmem;
+    ctx.join_next = (uint32_t *)((char *)dmem + ((jb + 255) & ~(size_t)255));
+    ctx.join_cap = (uint32_t)(scopes + 1);
+    ctx.result = (unsigned long long *)(ctx.join_next + 16);
+    HX_HIP(hipMemsetAsync(ctx.join_next, 0, 256, m.stream));
+    PoolView pool;
+    HX_TRY(make_pool((uint32_t)env_int("HCLIB_HIP_DEQUES", 64),
+                     (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
+                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 32), FibKind::kWords, &pool));
+    SchedConfig cfg;
+    cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_HI", 256);
+    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", 8);
+    cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
+    HX_TRY(reset_sched(pool, 1));
+    const int grid = m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 8);
+    HX_HIP(hipEventRecord(m.ev0, m.stream));
+    hipLaunchKernelGGL(k_fib, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
+    HX_HIP(hipGetLastError());
+    HX_HIP(hipEventRecord(m.ev1, m.stream));
+    SchedGlobals gl;
+    int rc = finish_sched(&gl, "hclib_hip_fib");
+    unsigned long long v = 0;
+    if (rc == HCLIB_HIP_OK) rc = hip_check(hipMemcpy(&v, ctx.result, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
+    (void)hipFree(dmem);
+    if (rc != HCLIB_HIP_OK) return rc;
+    *value = (int64_t)v;
+    if (result) {
+        result->tasks = gl.counters[0];
+        result->joins = gl.counters[1];
+        result->chunks_pushed = gl.counters[14];
+        result->chunks_stolen = gl.counters[15];
+        result->kernel_ms = ms;
+    }
+    return HCLIB_HIP_OK;
+}

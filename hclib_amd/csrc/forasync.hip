@@ -1,0 +1,301 @@
+// forasync.hip — hclib_forasync lowered to coalesced grid-stride tiles.
+//
+// The reference spawns one task per tile and calls the user function once
+// per index through a pointer (forasync1D_runner, src/hclib.c:110-120;
+// FLAT 316-351, RECURSIVE 158-190; 2-D/3-D 122-156, 192-314, 353-416). On the
+// GPU the tiles are not tasks: the exact iteration set of the requested mode
+// is described per dimension as a list of runs {first, count, stride} (one
+// run per reference tile, merged when contiguous), and a single launch
+// sweeps the cartesian product with consecutive lanes on consecutive
+// indices. The common case — stride 1, contiguous coverage, 1-D — is the
+// fast path: float4 grid-stride tiles with non-temporal stores (the HBM
+// roofline kernel of BASELINE config 1).
+#include <string.h>
+
+#include <vector>
+
+#include "hx_module.h"
+
+namespace hx {
+
+// ------------------------------------------------------- triad fast path
+// a[i] = b[i] + s*c[i], no contraction: __fmul_rn / __fadd_rn keep the
+// product rounded before the add, bit-identical to the CPU reference loop.
+__device__ __forceinline__ float triad1(float b, float c, float s) {
+    return __fadd_rn(b, __fmul_rn(s, c));
+}
+
+constexpr int kTriadThreads = 256;
+constexpr int kTriadUnroll = 4;  // float4 loads in flight per lane per operand
+
+__global__ __launch_bounds__(kTriadThreads) void k_triad_f32(float *__restrict__ a,
+                                                             const float *__restrict__ b,
+                                                             const float *__restrict__ c, float s,
+                                                             int64_t n4) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const int64_t stride = (int64_t)gridDim.x * kTriadThreads;
+    int64_t i = (int64_t)blockIdx.x * kTriadThreads + threadIdx.x;
+    const v4f *b4 = reinterpret_cast<const v4f *>(b);
+    const v4f *c4 = reinterpret_cast<const v4f *>(c);
+    v4f *a4 = reinterpret_cast<v4f *>(a);
+    // main loop: kTriadUnroll independent 16-B pairs per lane in flight
+    for (; i + (kTriadUnroll - 1) * stride < n4; i += kTriadUnroll * stride) {
+        v4f vb[kTriadUnroll], vc[kTriadUnroll];
+#pragma unroll
+        for (int u = 0; u < kTriadUnroll; ++u) {
+            vb[u] = __builtin_nontemporal_load(&b4[i + u * stride]);
+            vc[u] = __builtin_nontemporal_load(&c4[i + u * stride]);
+        }
+#pragma unroll
+        for (int u = 0; u < kTriadUnroll; ++u) {
+            v4f r;
+            r.x = triad1(vb[u].x, vc[u].x, s);
+            r.y = triad1(vb[u].y, vc[u].y, s);
+            r.z = triad1(vb[u].z, vc[u].z, s);
+            r.w = triad1(vb[u].w, vc[u].w, s);
+            __builtin_nontemporal_store(r, &a4[i + u * stride]);
+        }
+    }
+    for (; i < n4; i += stride) {
+        v4f vb = b4[i], vc = c4[i], r;
+        r.x = triad1(vb.x, vc.x, s);
+        r.y = triad1(vb.y, vc.y, s);
+        r.z = triad1(vb.z, vc.z, s);
+        r.w = triad1(vb.w, vc.w, s);
+        __builtin_nontemporal_store(r, &a4[i]);
+    }
+}
+
+__global__ void k_triad_tail(float *a, const float *b, const float *c, float s, int64_t from,
+                             int64_t n) {
+    int64_t i = from + threadIdx.x;
+    if (i < n) a[i] = triad1(b[i], c[i], s);
+}
+
+// -------------------------------------------------------- generic sweep
+struct Run {
+    int first;
+    int count;
+    int stride;
+    int pad;
+};
+
+struct DimRuns {
+    const Run *runs;
+    const int64_t *prefix;  // prefix[r] = iterations before run r; prefix[nruns] = total
+    int nruns;
+};
+
+struct SweepArgs {
+    DimRuns dim[3];
+    int ndim;
+    int64_t total;
+    int body;
+    hclib_hip_triad_args_t triad;
+    hclib_hip_iota_args_t iota;
+    hclib_hip_visit_args_t visit;
+};
+
+__device__ __forceinline__ int run_index(const DimRuns &d, int64_t t, int64_t &off) {
+    int lo = 0, hi = d.nruns - 1;
+    while (lo < hi) {  // last run with prefix <= t
+        int mid = (lo + hi + 1) >> 1;
+        if (d.prefix[mid] <= t) lo = mid;
+        else hi = mid - 1;
+    }
+    off = t - d.prefix[lo];
+    return lo;
+}
+
+__device__ __forceinline__ int idx_of(const DimRuns &d, int64_t t) {
+    int64_t off;
+    const Run r = d.runs[run_index(d, t, off)];
+    return r.first + (int)off * r.stride;
+}
+
+__global__ __launch_bounds__(256) void k_forasync_sweep(SweepArgs A) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    const int64_t n1 = A.ndim > 1 ? A.dim[1].prefix[A.dim[1].nruns] : 1;
+    const int64_t n2 = A.ndim > 2 ? A.dim[2].prefix[A.dim[2].nruns] : 1;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < A.total; t += step) {
+        // innermost dimension varies fastest -> consecutive lanes, consecutive indices
+        int64_t t2 = t % n2, r = t / n2;
+        int64_t t1 = r % n1, t0 = r / n1;
+        const int i = idx_of(A.dim[0], t0);
+        const int j = A.ndim > 1 ? idx_of(A.dim[1], t1) : 0;
+        const int k = A.ndim > 2 ? idx_of(A.dim[2], t2) : 0;
+        switch (A.body) {
+        case HCLIB_HIP_BODY_TRIAD_F32:
+            A.triad.a[i] = triad1(A.triad.b[i], A.triad.c[i], A.triad.s);
+            break;
+        case HCLIB_HIP_BODY_IOTA_CHECK:
+            if (A.iota.ran[i] != -1) atomicAdd(A.iota.errors, 1);
+            A.iota.ran[i] = i;
+            break;
+        case HCLIB_HIP_BODY_VISIT_COUNT: {
+            const hclib_hip_visit_args_t &v = A.visit;
+            const long li = (long)(i - v.base[0]), lj = (long)(j - v.base[1]),
+                       lk = (long)(k - v.base[2]);
+            if (li >= 0 && li < v.extent[0] && lj >= 0 && lj < v.extent[1] && lk >= 0 &&
+                lk < v.extent[2])
+                atomicAdd(&v.counts[(li * v.extent[1] + lj) * v.extent[2] + lk], 1);
+            break;
+        }
+        default:
+            break;
+        }
+    }
+}
+
+// -------------------------------------------------- host: iteration sets
+static void add_run(std::vector<Run> &v, int lo, int hi, int stride) {
+    if (hi <= lo) return;
+    const int cnt = (int)(((int64_t)hi - lo + stride - 1) / stride);
+    if (!v.empty() && stride == 1 && v.back().stride == 1 &&
+        v.back().first + v.back().count == lo) {
+        v.back().count += cnt;  // merge contiguous unit-stride tiles
+        return;
+    }
+    v.push_back(Run{lo, cnt, stride, 0});
+}
+
+// 1-D FLAT: forasync1D_flat, src/hclib.c:316-351 (chunks counted from 0)
+static void runs_flat1d(const hclib_hip_loop_domain_t &d, std::vector<Run> &v) {
+    const int nb_chunks = d.high / d.tile;
+    const int size = d.tile * nb_chunks;
+    int low0;
+    for (low0 = d.low; low0 < size; low0 += d.tile) add_run(v, low0, low0 + d.tile, d.stride);
+    if (size < d.high) add_run(v, low0, d.high, d.stride);
+}
+
+// per-dimension FLAT tiles of the 2-D/3-D lowering (src/hclib.c:353-416)
+static void runs_flat_nd(const hclib_hip_loop_domain_t &d, std::vector<Run> &v) {
+    for (int low0 = d.low; low0 < d.high; low0 += d.tile) {
+        const int high0 = (low0 + d.tile) > d.high ? d.high : (low0 + d.tile);
+        add_run(v, low0, high0, d.stride);
+    }
+}
+
+// RECURSIVE: bisection at mid=(high+low)/2 until <= tile (src/hclib.c:158-190,
+// 192-314); leaves in index order.
+static void runs_recursive(int low, int high, const hclib_hip_loop_domain_t &d,
+                           std::vector<Run> &v) {
+    if ((high - low) > d.tile) {
+        const int mid = (high + low) / 2;
+        runs_recursive(low, mid, d, v);
+        runs_recursive(mid, high, d, v);
+    } else {
+        add_run(v, low, high, d.stride);
+    }
+}
+
+}  // namespace hx
+
+using namespace hx;
+
+extern "C" int hclib_hip_forasync_triad_f32(float *a, const float *b, const float *c, float s,
+                                            int64_t n, void *stream) {
+    if (!a || !b || !c || n < 0) {
+        set_error("hclib_hip_forasync_triad_f32: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    hipStream_t st = (hipStream_t)stream;
+    const bool aligned = (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) & 15) == 0;
+    if (!aligned) {
+        set_error("hclib_hip_forasync_triad_f32: arrays must be 16-byte aligned");
+        return HCLIB_HIP_EINVAL;
+    }
+    const int64_t n4 = n / 4;
+    if (n4 > 0) {
+        const int bpc = env_int("HCLIB_HIP_TRIAD_BLOCKS_PER_CU", 8);
+        int64_t grid = (int64_t)mod().num_cus * bpc;
+        const int64_t need = (n4 + kTriadThreads - 1) / kTriadThreads;
+        if (grid > need) grid = need;
+        hipLaunchKernelGGL(k_triad_f32, dim3((unsigned)grid), dim3(kTriadThreads), 0, st, a, b, c,
+                           s, n4);
+        HX_HIP(hipGetLastError());
+    }
+    if (n4 * 4 < n) {
+        hipLaunchKernelGGL(k_triad_tail, dim3(1), dim3(64), 0, st, a, b, c, s, n4 * 4, n);
+        HX_HIP(hipGetLastError());
+    }
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_forasync(int body, const void *args, int dim,
+                                  hclib_hip_loop_domain_t *domain, int mode, void *stream) {
+    if (!args || !domain || dim < 1 || dim > 3 || (mode != 0 && mode != 1) ||
+        (body == HCLIB_HIP_BODY_TRIAD_F32 && dim != 1) ||
+        (body == HCLIB_HIP_BODY_IOTA_CHECK && dim != 1) || body < 1 || body > 3) {
+        set_error("hclib_hip_forasync: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    const int nworkers = hclib_hip_num_workers();
+    for (int d = 0; d < dim; ++d) {
+        if (domain[d].stride < 1) {
+            set_error("hclib_hip_forasync: stride must be >= 1");
+            return HCLIB_HIP_EINVAL;
+        }
+        if (domain[d].tile == -1)  // src/hclib.c:455-461, written back
+            domain[d].tile = ((domain[d].high - domain[d].low) + nworkers - 1) / nworkers;
+        if (domain[d].tile < 1) domain[d].tile = 1;
+    }
+    std::vector<Run> runs[3];
+    for (int d = 0; d < dim; ++d) {
+        if (mode == HCLIB_HIP_FORASYNC_RECURSIVE) runs_recursive(domain[d].low, domain[d].high, domain[d], runs[d]);
+        else if (dim == 1) runs_flat1d(domain[d], runs[d]);
+        else runs_flat_nd(domain[d], runs[d]);
+    }
+    // fast path: triad over one contiguous unit-stride run starting at 0
+    if (body == HCLIB_HIP_BODY_TRIAD_F32 && runs[0].size() == 1 && runs[0][0].stride == 1 &&
+        runs[0][0].first == 0) {
+        const hclib_hip_triad_args_t *t = (const hclib_hip_triad_args_t *)args;
+        return hclib_hip_forasync_triad_f32(t->a, t->b, t->c, t->s, runs[0][0].count, stream);
+    }
+    SweepArgs A;
+    memset(&A, 0, sizeof(A));
+    A.ndim = dim;
+    A.body = body;
+    if (body == HCLIB_HIP_BODY_TRIAD_F32) A.triad = *(const hclib_hip_triad_args_t *)args;
+    if (body == HCLIB_HIP_BODY_IOTA_CHECK) A.iota = *(const hclib_hip_iota_args_t *)args;
+    if (body == HCLIB_HIP_BODY_VISIT_COUNT) A.visit = *(const hclib_hip_visit_args_t *)args;
+    // upload runs + prefixes in one buffer
+    size_t bytes = 0;
+    std::vector<int64_t> pre[3];
+    A.total = 1;
+    for (int d = 0; d < dim; ++d) {
+        pre[d].resize(runs[d].size() + 1);
+        pre[d][0] = 0;
+        for (size_t r = 0; r < runs[d].size(); ++r) pre[d][r + 1] = pre[d][r] + runs[d][r].count;
+        if (runs[d].empty()) runs[d].push_back(Run{0, 0, 1, 0});
+        bytes += runs[d].size() * sizeof(Run) + pre[d].size() * 8 + 64;
+        A.total *= pre[d].back();
+    }
+    if (A.total == 0) return HCLIB_HIP_OK;
+    char *dbuf = nullptr;
+    HX_HIP(hipMalloc((void **)&dbuf, bytes));
+    std::vector<char> hbuf(bytes);
+    size_t off = 0;
+    for (int d = 0; d < dim; ++d) {
+        memcpy(&hbuf[off], runs[d].data(), runs[d].size() * sizeof(Run));
+        A.dim[d].runs = (const Run *)(dbuf + off);
+        off += (runs[d].size() * sizeof(Run) + 15) & ~(size_t)15;
+        memcpy(&hbuf[off], pre[d].data(), pre[d].size() * 8);
+        A.dim[d].prefix = (const int64_t *)(dbuf + off);
+        off += (pre[d].size() * 8 + 15) & ~(size_t)15;
+        A.dim[d].nruns = (int)runs[d].size();
+    }
+    hipStream_t st = (hipStream_t)stream;
+    HX_HIP(hipMemcpyAsync(dbuf, hbuf.data(), bytes, hipMemcpyHostToDevice, st));
+    int64_t grid = (A.total + 255) / 256;
+    const int64_t maxg = (int64_t)mod().num_cus * 16;
+    if (grid > maxg) grid = maxg;
+    hipLaunchKernelGGL(k_forasync_sweep, dim3((unsigned)grid), dim3(256), 0, st, A);
+    HX_HIP(hipGetLastError());
+    // the run table must outlive the launch
+    HX_HIP(hipStreamSynchronize(st));
+    HX_HIP(hipFree(dbuf));
+    return HCLIB_HIP_OK;
+}

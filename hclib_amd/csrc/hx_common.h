@@ -1,0 +1,117 @@
+// hx_common.h — shared device/host helpers for the MI355X hclib module.
+//
+// Inter-workgroup protocol (MI355X_MICROARCH.md "Workgroup dispatch, XCD
+// placement & inter-workgroup visibility", cdna_hip_programming.md G16):
+// every word another workgroup reads is written and read with agent-scope
+// atomics (global_* sc1: bypasses the per-CU L1, write-through past the
+// per-XCD L2), published behind `s_waitcnt vmcnt(0)` + an agent release
+// fence, and consumed after an agent acquire fence. Spins are bounded and
+// report through a device error word instead of hanging the GPU.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HX_AGENT __HIP_MEMORY_SCOPE_AGENT
+
+namespace hx {
+
+// ------------------------------------------------------------------ errors
+enum DevError : uint32_t {
+    kErrNone = 0,
+    kErrQueueFull = 1,
+    kErrStackOverflow = 2,
+    kErrSpinTimeout = 3,
+    kErrDepthTable = 4,
+    kErrArena = 5,
+    kErrBadTask = 6,
+};
+
+__device__ __forceinline__ void dev_error(uint32_t *err, uint32_t code) {
+    uint32_t zero = 0;
+    __hip_atomic_compare_exchange_strong(err, &zero, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         HX_AGENT);
+}
+
+// --------------------------------------------------------- agent atomics
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, HX_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, HX_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T add_agent(T *p, T v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, HX_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ bool cas_agent(T *p, T expected, T desired) {
+    return __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED,
+                                                __ATOMIC_RELAXED, HX_AGENT);
+}
+
+// Producer side of a hand-off: drain this wave's stores, then release.
+__device__ __forceinline__ void release_agent() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// Consumer side: invalidate this CU's L1 before reading handed-off bytes.
+__device__ __forceinline__ void acquire_agent() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ------------------------------------------------------------ wave utils
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// XCD (XCC) id of the executing CU: speed hint only, never correctness.
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_max_scan(int v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int t = __shfl_up(v, d, 64);
+        if (lane >= d) v = v > t ? v : t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_bcast(int v, int src) { return __shfl(v, src, 64); }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        T t = __shfl_xor(v, d, 64);
+        v = v > t ? v : t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void sleep_short() { __builtin_amdgcn_s_sleep(2); }
+
+}  // namespace hx

@@ -1,0 +1,51 @@
+// hx_module.h — host-side state of the MI355X `modules/hip` plug-in.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/hclib_hip.h"
+#include "hx_sched.h"
+
+namespace hx {
+
+// Per-process module state (one bound device per process, like one rank
+// per GPU in the multi-GPU launch).
+struct Module {
+    bool inited = false;
+    int device = -1;
+    int num_cus = 0;
+    std::string arch;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // chunk-deque arena, sized for the largest entry type, reused by launches
+    void *pool_mem = nullptr;
+    size_t pool_bytes = 0;
+    SchedGlobals *globals = nullptr;
+};
+
+Module &mod();
+void set_error(const char *fmt, ...);
+int ensure_device();  // HCLIB_HIP_OK or HCLIB_HIP_ENODEV
+int hip_check(hipError_t e, const char *what);
+
+// Carve a PoolView for `words` u32 per entry out of the arena (grows it).
+int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolView *out);
+// Reset the deques and the globals on the module stream before a launch.
+int reset_sched(const PoolView &pool, uint32_t outstanding_init);
+// Read back globals and translate the device error word.
+int finish_sched(SchedGlobals *host_copy, const char *who);
+
+// Environment knobs (HCLIB_HIP_WAVES_PER_CU, ...) with defaults.
+int env_int(const char *name, int dflt);
+
+}  // namespace hx
+
+#define HX_TRY(expr)                         \
+    do {                                     \
+        int _rc = (expr);                    \
+        if (_rc != HCLIB_HIP_OK) return _rc; \
+    } while (0)
+#define HX_HIP(call) HX_TRY(::hx::hip_check((call), #call))

@@ -1,0 +1,361 @@
+// hx_sched.h — the persistent work-stealing megakernel (device side).
+//
+// Replaces HClib's pthread worker loop and deques (src/hclib-runtime.c:646-729
+// core_work_loop/find_and_run_task, src/hclib-deque.c:50-139) with a
+// wavefront-granular scheduler:
+//
+//   worker        = one 64-lane wave (one workgroup of 64 threads), resident
+//                   for the whole launch; ~8 per CU.
+//   local deque   = a ring of task entries in the wave's LDS (the "LDS-cached
+//                   hot end"); the owner pushes/pops at the top (LIFO,
+//                   work-first like ss_get_work, test/uts/UTS.cpp:383-402).
+//   spill/steal   = the oldest entries of a ring move, as one chunk, into an
+//                   HBM chunk deque (bounded MPMC ring, one per XCD slice);
+//                   idle waves take chunks from their own deque first, then
+//                   from deques of the same XCD, then anywhere — the
+//                   reference's intra-socket-first victim order
+//                   (src/hclib-locality-graph.c:864-884) mapped to XCDs.
+//   a "task"      = one lane-item: an entry carries a count of items
+//                   (children to spawn, or 1), the wave expands up to 64
+//                   items per batch (one per lane) by prefix sum.
+//   termination   = `outstanding` = chunks in deques + waves holding work;
+//                   the launch ends when it reads 0 (the finish counter of
+//                   src/hclib-runtime.c:431-446 for the whole launch).
+//
+// All cross-wave words use agent-scope atomics; chunk payloads are written
+// with sc1 stores and published behind s_waitcnt + release, consumed after an
+// acquire (hx_common.h). Every spin is bounded.
+#pragma once
+
+#include "hx_common.h"
+
+namespace hx {
+
+constexpr int kWaveSize = 64;
+
+// One HBM chunk deque header, head and tail on separate 128-B lines.
+struct alignas(256) QueueHdr {
+    uint32_t head;
+    uint32_t pad0[31];
+    uint32_t tail;
+    uint32_t pad1[31];
+};
+
+// Global scheduler state shared by all waves of one launch (device memory).
+struct alignas(256) SchedGlobals {
+    uint32_t outstanding;  // chunks queued + waves holding work
+    uint32_t pad0[63];
+    uint32_t idle;  // waves currently without work (spill hint)
+    uint32_t pad1[63];
+    uint32_t err;  // DevError
+    uint32_t pad2[63];
+    unsigned long long counters[16];  // kind-specific reductions (atomic adds)
+    unsigned long long maxes[4];      // kind-specific reductions (atomic max)
+};
+
+struct PoolView {
+    QueueHdr *hdr;    // nq headers
+    uint32_t *seq;    // nq * cap sequence words
+    uint32_t *cnt;    // nq * cap entry counts
+    uint32_t *data;   // nq * cap * chunk * words
+    uint32_t nq;      // number of deques (multiple of 8)
+    uint32_t cap;     // slots per deque (power of two)
+    uint32_t chunk;   // entries per chunk (<= 64)
+};
+
+struct SchedConfig {
+    uint32_t spill_hi;   // always spill above this many entries
+    uint32_t spill_lo;   // spill above this when some wave is idle
+    uint32_t spin_limit; // ms a wave may stay idle before declaring a timeout
+};
+
+// Kind concept:
+//   static constexpr int kWords;      // u32 words per entry; word kWords-1 = start
+//   static constexpr int kMaxOut;     // entries one item may push
+//   struct Ctx;                       // per-launch read-only parameters
+//   struct Acc { ...; __device__ void flush(SchedGlobals*); };  // per-lane stats
+//   __device__ static uint32_t count(const uint32_t *e);        // items in entry
+//   __device__ static int process(const Ctx&, Acc&, const uint32_t *e, uint32_t k,
+//                                 uint32_t (*out)[kWords], uint32_t *err);
+//   __device__ static int roots(const Ctx&, Acc&, uint32_t (*out)[kWords]);  // wave 0 only
+
+template <class Kind, int CAP>
+struct WaveStack {
+    static constexpr int W = Kind::kWords;
+    uint32_t e[CAP][W];
+    int own[kWaveSize];
+};
+
+// Try to publish `n` entries (ring positions bot..bot+n-1) as one chunk into
+// deque q. Called by the whole wave; returns true if published.
+template <class Kind, int CAP>
+__device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
+                              WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n) {
+    constexpr int W = Kind::kWords;
+    const int lane = lane_id();
+    QueueHdr *h = &pool.hdr[q];
+    uint32_t pos = 0;
+    int ok = 0;
+    if (lane == 0) {
+        pos = ld_agent(&h->tail);
+        for (int it = 0; it < 64; ++it) {
+            uint32_t s = ld_agent(&pool.seq[q * pool.cap + (pos & (pool.cap - 1))]);
+            int dif = (int)(s - pos);
+            if (dif == 0) {
+                if (cas_agent(&h->tail, pos, pos + 1)) { ok = 1; break; }
+                pos = ld_agent(&h->tail);
+            } else if (dif < 0) {
+                break;  // full
+            } else {
+                pos = ld_agent(&h->tail);
+            }
+        }
+    }
+    ok = __shfl(ok, 0, 64);
+    if (!ok) return false;
+    pos = __shfl(pos, 0, 64);
+    const uint32_t slot = q * pool.cap + (pos & (pool.cap - 1));
+    uint32_t *dst = pool.data + (size_t)slot * pool.chunk * W;
+    // the reservation counts as outstanding work before it becomes visible
+    if (lane == 0) add_agent(&g->outstanding, 1u);
+    for (uint32_t i = lane; i < n * W; i += kWaveSize) {
+        uint32_t ent = i / W, w = i % W;
+        st_agent(&dst[i], st.e[(bot + ent) & (CAP - 1)][w]);
+    }
+    if (lane == 0) st_agent(&pool.cnt[slot], n);
+    release_agent();
+    if (lane == 0) st_agent(&pool.seq[slot], pos + 1);
+    return true;
+}
+
+// Try to take one chunk from deque q into the (empty) stack. Returns the
+// number of entries taken (0 if the deque looked empty).
+template <class Kind, int CAP>
+__device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Kind, CAP> &st) {
+    constexpr int W = Kind::kWords;
+    const int lane = lane_id();
+    QueueHdr *h = &pool.hdr[q];
+    uint32_t pos = 0;
+    int ok = 0;
+    if (lane == 0) {
+        pos = ld_agent(&h->head);
+        for (int it = 0; it < 16; ++it) {
+            uint32_t s = ld_agent(&pool.seq[q * pool.cap + (pos & (pool.cap - 1))]);
+            int dif = (int)(s - (pos + 1));
+            if (dif == 0) {
+                if (cas_agent(&h->head, pos, pos + 1)) { ok = 1; break; }
+                pos = ld_agent(&h->head);
+            } else if (dif < 0) {
+                break;  // empty (or the producer has not published yet)
+            } else {
+                pos = ld_agent(&h->head);
+            }
+        }
+    }
+    ok = __shfl(ok, 0, 64);
+    if (!ok) return 0;
+    pos = __shfl(pos, 0, 64);
+    acquire_agent();
+    const uint32_t slot = q * pool.cap + (pos & (pool.cap - 1));
+    const uint32_t n = ld_agent(&pool.cnt[slot]);
+    const uint32_t *src = pool.data + (size_t)slot * pool.chunk * W;
+    for (uint32_t i = lane; i < n * W; i += kWaveSize) {
+        uint32_t ent = i / W, w = i % W;
+        st.e[ent][w] = ld_agent(&src[i]);
+    }
+    // all reads of the slot have landed before it is handed back
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) st_agent(&pool.seq[slot], pos + pool.cap);
+    __syncthreads();  // one wave per workgroup: orders the LDS ring writes
+    return n;
+}
+
+__device__ __forceinline__ uint32_t xorshift(uint32_t &s) {
+    s ^= s << 13;
+    s ^= s >> 17;
+    s ^= s << 5;
+    return s;
+}
+
+template <class Kind, int CAP>
+__device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, SchedGlobals *g,
+                           const SchedConfig &cfg, WaveStack<Kind, CAP> &st, bool seed_roots) {
+    constexpr int W = Kind::kWords;
+    constexpr int MO = Kind::kMaxOut;
+    static_assert((CAP & (CAP - 1)) == 0, "CAP must be a power of two");
+    const int lane = lane_id();
+    const uint32_t gid = blockIdx.x;
+    const uint32_t nxcd = 8;
+    const uint32_t qpx = pool.nq / nxcd;
+    const uint32_t xcc = xcc_id() & 7u;
+    const uint32_t home = xcc * qpx + (gid / nxcd) % qpx;
+    uint32_t rng = 0x9e3779b9u ^ (gid * 0x85ebca6bu + 1u);
+
+    typename Kind::Acc acc;
+    uint32_t bot = 0, top = 0;
+    bool active = false;
+    uint32_t spins = 0;
+    unsigned long long idle_since = 0;
+    unsigned long long nbatch = 0, npush = 0, nsteal = 0;
+
+    if (seed_roots) {
+        uint32_t out[MO > 4 ? MO : 4][W];
+        int n = Kind::roots(ctx, acc, out);
+        // roots() is uniform across the wave; lane 0's view is authoritative
+        if (lane == 0)
+            for (int i = 0; i < n; ++i)
+                for (int w = 0; w < W; ++w) st.e[i][w] = out[i][w];
+        top = n;
+        active = true;  // the host initialised outstanding = 1 for this wave
+        if (n == 0) {
+            active = false;
+            if (lane == 0) __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+        }
+        __syncthreads();
+    }
+    if (!active && lane == 0) add_agent(&g->idle, 1u);
+
+    while (true) {
+        const uint32_t size = top - bot;
+        if (size == 0) {
+            if (active) {
+                active = false;
+                if (lane == 0) {
+                    add_agent(&g->idle, 1u);
+                    __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+                }
+            }
+            // try home deque, then a random deque (3/4 same XCD, 1/4 anywhere)
+            uint32_t q = home;
+            if (spins & 1) {
+                uint32_t r = xorshift(rng);
+                r = __shfl(r, 0, 64);
+                if ((r & 3) != 0) q = xcc * qpx + (r >> 2) % qpx;
+                else q = (r >> 2) % pool.nq;
+            }
+            uint32_t n = dequeue_chunk<Kind, CAP>(pool, q, st);
+            if (n) {
+                if (q != home) ++nsteal;
+                bot = 0;
+                top = n;
+                active = true;
+                spins = 0;
+                if (lane == 0) add_agent(&g->idle, (uint32_t)-1);
+                continue;
+            }
+            uint32_t outst = 0;
+            if (lane == 0) outst = ld_agent(&g->outstanding);
+            outst = __shfl(outst, 0, 64);
+            if (outst == 0) break;
+            uint32_t e = 0;
+            if (lane == 0) e = ld_agent(&g->err);
+            if (__shfl(e, 0, 64)) break;
+            // bounded idle: 100 MHz constant clock, cfg.spin_limit in ms
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            if (spins++ == 0) idle_since = now;
+            else if (now - idle_since > 100000ull * cfg.spin_limit) {
+                if (lane == 0) dev_error(&g->err, kErrSpinTimeout);
+                break;
+            }
+            // back off: 64*2^k cycles, capped, so idle pollers do not
+            // saturate the deque heads the working waves need
+            if (spins < 4) __builtin_amdgcn_s_sleep(1);
+            else if (spins < 16) __builtin_amdgcn_s_sleep(4);
+            else __builtin_amdgcn_s_sleep(16);
+            continue;
+        }
+        ++nbatch;
+        // ---- form a batch of up to 64 items from the top entries
+        uint32_t cnt = 0, start = 0, eidx = 0;
+        if ((uint32_t)lane < size) {
+            eidx = (top - 1 - lane) & (CAP - 1);
+            start = st.e[eidx][W - 1];
+            cnt = Kind::count(st.e[eidx]) - start;
+        }
+        const int S = wave_incl_scan((int)cnt);
+        const int total = __shfl(S, 63, 64);
+        const int take = total < kWaveSize ? total : kWaveSize;
+        const int excl = S - (int)cnt;
+        st.own[lane] = -1;
+        __syncthreads();
+        if (cnt > 0 && excl < kWaveSize) st.own[excl] = lane;
+        __syncthreads();
+        const int owner = wave_incl_max_scan(st.own[lane]);
+        const int owner_excl = __shfl(excl, owner < 0 ? 0 : owner, 64);
+        const uint32_t owner_e = __shfl(eidx, owner < 0 ? 0 : owner, 64);
+        const uint32_t owner_start = __shfl(start, owner < 0 ? 0 : owner, 64);
+        uint32_t out[MO][W];
+        int nout = 0;
+        if (lane < take) {
+            uint32_t ent[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) ent[w] = st.e[owner_e][w];
+            const uint32_t k = owner_start + (uint32_t)(lane - owner_excl);
+            nout = Kind::process(ctx, acc, ent, k, out, &g->err);
+        }
+        __syncthreads();  // every lane has read its entry before the ring changes
+        // ---- retire consumed entries (all reads of them happened above)
+        const bool full = ((uint32_t)lane < size) && S <= take;  // (0-count entries retire too)
+        const uint32_t nfull = __popcll(__ballot(full));
+        // entry just below the fully consumed ones may be partially consumed
+        if ((uint32_t)lane == nfull && (uint32_t)lane < size && excl < take)
+            st.e[eidx][W - 1] = start + (uint32_t)(take - excl);
+        top -= nfull;
+        // ---- push outputs
+        const int P = wave_incl_scan(nout);
+        const int tout = __shfl(P, 63, 64);
+        if ((top - bot) + (uint32_t)tout > (uint32_t)CAP) {
+            if (lane == 0) dev_error(&g->err, kErrStackOverflow);
+            break;
+        }
+        {
+            uint32_t p = top + (uint32_t)(P - nout);
+            for (int o = 0; o < nout; ++o, ++p)
+#pragma unroll
+                for (int w = 0; w < W; ++w) st.e[p & (CAP - 1)][w] = out[o][w];
+        }
+        top += (uint32_t)tout;
+        __syncthreads();
+        // ---- spill the oldest entries when the ring is large, or when
+        //      some wave is idle and we hold more than spill_lo entries
+        uint32_t sz = top - bot;
+        if (sz > cfg.spill_lo) {
+            uint32_t idle = 0;
+            if (lane == 0) idle = ld_agent(&g->idle);
+            idle = __shfl(idle, 0, 64);
+            while (sz > cfg.spill_hi || (idle > 0 && sz > cfg.spill_lo)) {
+                uint32_t n = sz / 2;
+                if (n > pool.chunk) n = pool.chunk;
+                if (n == 0) break;
+                // home deque first, then the other deques of this XCD slice
+                bool ok = false;
+                for (uint32_t a = 0; a < 4 && !ok; ++a) {
+                    const uint32_t q = (a == 0) ? home : xcc * qpx + (home + a) % qpx;
+                    ok = enqueue_chunk<Kind, CAP>(pool, g, q, st, bot, n);
+                }
+                if (!ok) {
+                    if (sz > (uint32_t)(CAP - kWaveSize * MO)) {
+                        if (lane == 0) dev_error(&g->err, kErrQueueFull);
+                    }
+                    break;
+                }
+                ++npush;
+                bot += n;
+                sz = top - bot;
+                if (idle) --idle;
+            }
+        }
+    }
+    if (active && lane == 0) {
+        // only reached on an error break: keep the protocol consistent
+        __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+    }
+    acc.flush(g);
+    if (lane == 0) {
+        add_agent(&g->counters[13], nbatch);
+        add_agent(&g->counters[14], npush);
+        add_agent(&g->counters[15], nsteal);
+    }
+}
+
+}  // namespace hx

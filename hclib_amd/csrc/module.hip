@@ -1,0 +1,174 @@
+// module.hip — `modules/hip` lifecycle, error reporting and the shared
+// chunk-deque arena (the HBM side of the per-wave deques, sched.h).
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "hx_module.h"
+
+namespace hx {
+
+static Module g_mod;
+static thread_local char g_err[512] = "";
+
+Module &mod() { return g_mod; }
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int hip_check(hipError_t e, const char *what) {
+    if (e == hipSuccess) return HCLIB_HIP_OK;
+    set_error("%s failed: %s", what, hipGetErrorString(e));
+    return HCLIB_HIP_EHIP;
+}
+
+int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+int ensure_device() {
+    if (g_mod.inited) return HCLIB_HIP_OK;
+    return hclib_hip_init(env_int("HCLIB_HIP_DEVICE", 0)) == HCLIB_HIP_OK ? HCLIB_HIP_OK
+                                                                           : HCLIB_HIP_ENODEV;
+}
+
+__global__ void k_reset_pool(uint32_t *seq, uint32_t cap, uint32_t total) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < total) seq[i] = i & (cap - 1);
+}
+
+int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolView *out) {
+    const size_t hdr = sizeof(QueueHdr) * nq;
+    const size_t slots = (size_t)nq * cap;
+    const size_t need = hdr + slots * 4 * 2 + slots * chunk * words * 4 + 4096;
+    Module &m = g_mod;
+    if (need > m.pool_bytes) {
+        if (m.pool_mem) (void)hipFree(m.pool_mem);
+        m.pool_mem = nullptr;
+        m.pool_bytes = 0;
+        if (hipMalloc(&m.pool_mem, need) != hipSuccess) {
+            set_error("hipMalloc(%zu) for the chunk deques failed", need);
+            return HCLIB_HIP_ENOMEM;
+        }
+        m.pool_bytes = need;
+    }
+    char *p = (char *)m.pool_mem;
+    out->hdr = (QueueHdr *)p;
+    p += hdr;
+    out->seq = (uint32_t *)p;
+    p += slots * 4;
+    out->cnt = (uint32_t *)p;
+    p += slots * 4;
+    p = (char *)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+    out->data = (uint32_t *)p;
+    out->nq = nq;
+    out->cap = cap;
+    out->chunk = chunk;
+    return HCLIB_HIP_OK;
+}
+
+int reset_sched(const PoolView &pool, uint32_t outstanding_init) {
+    Module &m = g_mod;
+    HX_HIP(hipMemsetAsync(pool.hdr, 0, sizeof(QueueHdr) * pool.nq, m.stream));
+    const uint32_t total = pool.nq * pool.cap;
+    hipLaunchKernelGGL(k_reset_pool, dim3((total + 255) / 256), dim3(256), 0, m.stream, pool.seq,
+                       pool.cap, total);
+    HX_HIP(hipGetLastError());
+    SchedGlobals init;
+    memset(&init, 0, sizeof(init));
+    init.outstanding = outstanding_init;
+    HX_HIP(hipMemcpyAsync(m.globals, &init, sizeof(init), hipMemcpyHostToDevice, m.stream));
+    return HCLIB_HIP_OK;
+}
+
+static const char *err_name(uint32_t e) {
+    switch (e) {
+    case kErrQueueFull: return "chunk deque full and LDS ring near capacity";
+    case kErrStackOverflow: return "LDS ring overflow";
+    case kErrSpinTimeout: return "idle spin timed out (no termination)";
+    case kErrDepthTable: return "tree deeper than the device depth-rule table";
+    case kErrArena: return "device arena exhausted";
+    case kErrBadTask: return "malformed task";
+    default: return "unknown device error";
+    }
+}
+
+int finish_sched(SchedGlobals *host_copy, const char *who) {
+    Module &m = g_mod;
+    HX_HIP(hipMemcpyAsync(host_copy, m.globals, sizeof(SchedGlobals), hipMemcpyDeviceToHost,
+                          m.stream));
+    HX_HIP(hipStreamSynchronize(m.stream));
+    if (host_copy->err) {
+        set_error("%s: device error %u (%s)", who, host_copy->err, err_name(host_copy->err));
+        return HCLIB_HIP_EDEVICE;
+    }
+    return HCLIB_HIP_OK;
+}
+
+}  // namespace hx
+
+using namespace hx;
+
+extern "C" {
+
+const char *hclib_hip_version(void) { return "hclib-mi355x 0.1 (gfx950 megakernel scheduler)"; }
+
+const char *hclib_hip_last_error(void) { return g_err; }
+
+int hclib_hip_init(int device) {
+    Module &m = g_mod;
+    if (m.inited) return HCLIB_HIP_OK;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_error("hclib_hip_init: no HIP device visible");
+        return HCLIB_HIP_ENODEV;
+    }
+    if (device < 0 || device >= n) {
+        set_error("hclib_hip_init: device %d out of range (%d devices)", device, n);
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HX_HIP(hipGetDeviceProperties(&prop, device));
+    m.arch = prop.gcnArchName;
+    if (m.arch.rfind("gfx950", 0) != 0) {
+        set_error("hclib_hip_init: device %d is %s, this module is built for gfx950 only", device,
+                  prop.gcnArchName);
+        return HCLIB_HIP_ENODEV;
+    }
+    m.device = device;
+    m.num_cus = prop.multiProcessorCount;
+    HX_HIP(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
+    HX_HIP(hipEventCreate(&m.ev0));
+    HX_HIP(hipEventCreate(&m.ev1));
+    HX_HIP(hipMalloc((void **)&m.globals, sizeof(SchedGlobals)));
+    m.inited = true;
+    return HCLIB_HIP_OK;
+}
+
+void hclib_hip_finalize(void) {
+    Module &m = g_mod;
+    if (!m.inited) return;
+    (void)hipStreamSynchronize(m.stream);
+    if (m.pool_mem) (void)hipFree(m.pool_mem);
+    (void)hipFree(m.globals);
+    (void)hipEventDestroy(m.ev0);
+    (void)hipEventDestroy(m.ev1);
+    (void)hipStreamDestroy(m.stream);
+    m = Module();
+}
+
+int hclib_hip_num_cus(void) { return g_mod.inited ? g_mod.num_cus : 0; }
+
+int hclib_hip_num_workers(void) {
+    if (!g_mod.inited) return 0;
+    return g_mod.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 8);
+}
+
+}  // extern "C"

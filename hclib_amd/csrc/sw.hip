@@ -1,0 +1,309 @@
+// sw.hip — the Smith-Waterman tile DAG (test/smithwaterman/smith_waterman.cpp)
+// with device-side dependency counters.
+//
+// Reference: every tile is an async_await on three futures (:227-229); each
+// completed tile puts three promises (bottom_right, right_column,
+// bottom_row, :212-226) and hclib_promise_put walks the waiter lists
+// (src/hclib-promise.c:203-245) to make dependants runnable.
+// Here: a tile's three futures are one dependency counter (boundary
+// promises are pre-satisfied, :141-165, so border tiles start lower); a
+// finished tile publishes its bottom row / right column / corner with
+// write-through stores, releases, then decrements each dependant's counter;
+// the decrement that reaches zero appends the dependant to a ready list.
+// Persistent waves take tickets on the ready list in order (one agent
+// atomic) — every ticket below the tile count is eventually filled because
+// the DAG is acyclic, so the wait is bounded and deadlock-free.
+//
+// In-tile DP: one wave per tile; lane L owns RP consecutive rows of a
+// 64*RP-row band and sweeps the columns skewed by L (anti-diagonal
+// pipeline): at step s it computes column s-L, receiving the cell above from
+// lane L-1 through a one-lane DPP shift. Bands are chained through LDS.
+#include <string.h>
+
+#include <vector>
+
+#include "hx_module.h"
+
+namespace hx {
+
+constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr int kSwRP = 4;  // rows per lane per band -> 256-row bands
+
+struct SwCtx {
+    const int8_t *s1;  // coded 1..4
+    const int8_t *s2;
+    int tw, th, ntw, nth;
+    int *bottom;       // [tiles][tw]
+    int *right;        // [tiles][th]
+    int *corner;       // [tiles]
+    uint32_t *deps;    // [tiles]
+    uint32_t *ready;   // [tiles] ticket-ordered ready list (kEmpty = not yet)
+    uint32_t *ready_tail;
+    uint32_t *ready_head;
+    uint32_t *err;
+    unsigned long long *stats;  // [0] tiles, [1] releases
+    uint32_t spin_ms;
+};
+
+// alignment_score_matrix (smith_waterman.cpp:36-43) row for s2 code a,
+// packed as four signed bytes for s1 = 1..4
+__device__ __forceinline__ uint32_t sw_row(int a) {
+    // A: 2 -4 -2 -4 | C: -4 2 -4 -2 | G: -2 -4 2 -4 | T: -4 -2 -4 2
+    return a == 1 ? 0xfcfefc02u : a == 2 ? 0xfefc02fcu : a == 3 ? 0xfc02fcfeu : 0x02fcfefcu;
+}
+__device__ __forceinline__ int sw_m(uint32_t row, int b) {
+    return (int)(int8_t)(row >> (8 * (b - 1)));
+}
+
+__device__ __forceinline__ int shift_up1(int v) {
+    // lane L receives lane L-1's value (lane 0 receives garbage; it reads LDS)
+    return __shfl_up(v, 1, 64);
+}
+
+__device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, int8_t *lds_s1) {
+    const int lane = lane_id();
+    const int i = (int)(t / (uint32_t)c.ntw) + 1;  // tile row (1-based)
+    const int j = (int)(t % (uint32_t)c.ntw) + 1;  // tile col
+    const int tw = c.tw, th = c.th;
+    const uint32_t tup = t - (uint32_t)c.ntw, tleft = t - 1, tdiag = t - (uint32_t)c.ntw - 1;
+    // s1 segment of this tile column
+    for (int q = lane; q < tw; q += 64) lds_s1[q] = c.s1[(size_t)(j - 1) * tw + q];
+    // top row (row -1 of the tile, columns 0..tw): corner + above tile bottom row
+    if (lane == 0) {
+        lds_top[0] = (i == 1) ? -((j - 1) * tw) : (j == 1 ? -((i - 1) * th) : ld_agent(&c.corner[tdiag]));
+        if (i == 1 && j == 1) lds_top[0] = 0;
+    }
+    for (int q = lane; q < tw; q += 64)
+        lds_top[q + 1] = (i == 1) ? -((j - 1) * tw + q + 1) : ld_agent(&c.bottom[(size_t)tup * tw + q]);
+    __syncthreads();
+    for (int r0 = 0; r0 < th; r0 += 64 * kSwRP) {
+        const int rfirst = r0 + lane * kSwRP;
+        int left[kSwRP];
+        uint32_t mrow[kSwRP];
+        int nvalid = 0;
+#pragma unroll
+        for (int q = 0; q < kSwRP; ++q) {
+            const int r = rfirst + q;
+            if (r < th) {
+                ++nvalid;
+                left[q] = (j == 1) ? -((i - 1) * th + r + 1) : ld_agent(&c.right[(size_t)tleft * th + r]);
+                mrow[q] = sw_row(c.s2[(size_t)(i - 1) * th + r]);
+            } else {
+                left[q] = 0;
+                mrow[q] = 0;
+            }
+        }
+        // H[rfirst-1][0]: the left boundary one row up (corner for row 0)
+        int up_prev;
+        if (rfirst == 0) up_prev = lds_top[0];
+        else if (j == 1) up_prev = -((i - 1) * th + rfirst);
+        else up_prev = (rfirst - 1 < th) ? ld_agent(&c.right[(size_t)tleft * th + rfirst - 1]) : 0;
+        const int band_rows = (th - r0) < 64 * kSwRP ? (th - r0) : 64 * kSwRP;
+        const int last_lane = (band_rows - 1) / kSwRP;
+        const int last_q = (band_rows - 1) % kSwRP;
+        if (lane == last_lane) lds_bot[0] = left[last_q];  // H[band last row][0]
+        int out = 0;
+        const int steps = tw + 63;
+        for (int s = 0; s < steps; ++s) {
+            const int recv = shift_up1(out);
+            const int cidx = s - lane;  // 0-based column
+            if (cidx >= 0 && cidx < tw && nvalid > 0) {
+                int up = (lane == 0) ? lds_top[cidx + 1] : recv;
+                int diag = up_prev;
+                up_prev = up;
+                const int b = lds_s1[cidx];
+#pragma unroll
+                for (int q = 0; q < kSwRP; ++q) {
+                    const int dsc = diag + sw_m(mrow[q], b);
+                    const int l = left[q] - 1;
+                    const int u = up - 1;
+                    const int lt = l > u ? l : u;
+                    const int h = lt > dsc ? lt : dsc;
+                    diag = left[q];
+                    left[q] = h;
+                    up = h;
+                }
+                out = up;
+                if (lane == last_lane) lds_bot[cidx + 1] = left[last_q];
+                if (cidx == tw - 1) {
+#pragma unroll
+                    for (int q = 0; q < kSwRP; ++q)
+                        if (q < nvalid) st_agent(&c.right[(size_t)t * th + rfirst + q], left[q]);
+                }
+            }
+        }
+        __syncthreads();
+        // the band's bottom row becomes the next band's top row
+        for (int q = lane; q <= tw; q += 64) lds_top[q] = lds_bot[q];
+        __syncthreads();
+    }
+    for (int q = lane; q < tw; q += 64) st_agent(&c.bottom[(size_t)t * tw + q], lds_top[q + 1]);
+    if (lane == 0) st_agent(&c.corner[t], lds_top[tw]);
+}
+
+__global__ __launch_bounds__(64) void k_sw(SwCtx c) {
+    extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+    int *lds_top = sw_lds;
+    int *lds_bot = sw_lds + ((c.tw + 1 + 3) & ~3);
+    int8_t *lds_s1 = (int8_t *)(lds_bot + ((c.tw + 1 + 3) & ~3));
+    const int lane = lane_id();
+    const uint32_t ntiles = (uint32_t)(c.ntw * c.nth);
+    unsigned long long ntile = 0, nrel = 0;
+    while (true) {
+        uint32_t ticket = 0;
+        if (lane == 0) ticket = add_agent(c.ready_head, 1u);
+        ticket = __shfl(ticket, 0, 64);
+        if (ticket >= ntiles) break;
+        uint32_t t = kEmpty;
+        if (lane == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while ((t = ld_agent(&c.ready[ticket])) == kEmpty) {
+                if (ld_agent(c.err)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
+                    dev_error(c.err, kErrSpinTimeout);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        t = __shfl(t, 0, 64);
+        if (t == kEmpty) break;
+        acquire_agent();
+        __syncthreads();
+        sw_tile(c, t, lds_top, lds_bot, lds_s1);
+        ++ntile;
+        release_agent();  // every store of this tile drained and released
+        if (lane == 0) {
+            const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
+            const uint32_t succ[3] = {t + 1, t + (uint32_t)c.ntw, t + (uint32_t)c.ntw + 1};
+            const bool ok[3] = {j + 1 < c.ntw, i + 1 < c.nth, j + 1 < c.ntw && i + 1 < c.nth};
+            for (int k = 0; k < 3; ++k) {
+                if (!ok[k]) continue;
+                ++nrel;
+                const uint32_t old = __hip_atomic_fetch_add(&c.deps[succ[k]], (uint32_t)-1,
+                                                            __ATOMIC_ACQ_REL, HX_AGENT);
+                if (old == 1) {
+                    const uint32_t pos = add_agent(c.ready_tail, 1u);
+                    __hip_atomic_store(&c.ready[pos], succ[k], __ATOMIC_RELEASE, HX_AGENT);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (lane == 0) {
+        add_agent(&c.stats[0], ntile);
+        add_agent(&c.stats[1], nrel);
+    }
+}
+
+__global__ void k_sw_init(uint32_t *deps, uint32_t *ready, int ntw, int nth) {
+    const uint32_t n = (uint32_t)(ntw * nth);
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const int i = (int)(t / ntw), j = (int)(t % ntw);
+        deps[t] = (uint32_t)((i > 0) + (j > 0) + (i > 0 && j > 0));
+        ready[t] = (t == 0) ? 0u : kEmpty;
+    }
+}
+
+}  // namespace hx
+
+using namespace hx;
+
+extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_t n2, int tw,
+                            int th, int *score, hclib_hip_sw_result_t *result) {
+    if (!s1 || !s2 || !score || tw < 1 || th < 1 || tw > 16384) {
+        set_error("hclib_hip_sw: invalid arguments (1 <= tw <= 16384, th >= 1)");
+        return HCLIB_HIP_EINVAL;
+    }
+    const size_t ntw = n1 / (size_t)tw, nth = n2 / (size_t)th;
+    if (ntw == 0 || nth == 0 || ntw * nth > 0x7fffffffull) {
+        set_error("hclib_hip_sw: empty or oversized tile grid");
+        return HCLIB_HIP_EINVAL;
+    }
+    for (size_t k = 0; k < ntw * (size_t)tw; ++k)
+        if (s1[k] < 1 || s1[k] > 4) { set_error("hclib_hip_sw: s1 must be coded 1..4"); return HCLIB_HIP_EINVAL; }
+    for (size_t k = 0; k < nth * (size_t)th; ++k)
+        if (s2[k] < 1 || s2[k] > 4) { set_error("hclib_hip_sw: s2 must be coded 1..4"); return HCLIB_HIP_EINVAL; }
+    HX_TRY(ensure_device());
+    Module &m = mod();
+    const size_t nt = ntw * nth;
+    const size_t b_s1 = ntw * tw, b_s2 = nth * th;
+    const size_t b_bot = nt * tw * 4, b_right = nt * th * 4, b_c = nt * 4, b_dep = nt * 4,
+                 b_ready = nt * 4;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t total = al(b_s1) + al(b_s2) + al(b_bot) + al(b_right) + al(b_c) + al(b_dep) +
+                         al(b_ready) + 1024;
+    char *d = nullptr;
+    if (hipMalloc((void **)&d, total) != hipSuccess) {
+        set_error("hclib_hip_sw: hipMalloc(%zu) failed", total);
+        return HCLIB_HIP_ENOMEM;
+    }
+    SwCtx c;
+    size_t off = 0;
+    c.s1 = (const int8_t *)(d + off); off += al(b_s1);
+    c.s2 = (const int8_t *)(d + off); off += al(b_s2);
+    c.bottom = (int *)(d + off); off += al(b_bot);
+    c.right = (int *)(d + off); off += al(b_right);
+    c.corner = (int *)(d + off); off += al(b_c);
+    c.deps = (uint32_t *)(d + off); off += al(b_dep);
+    c.ready = (uint32_t *)(d + off); off += al(b_ready);
+    uint32_t *misc = (uint32_t *)(d + off);
+    c.ready_tail = misc;
+    c.ready_head = misc + 64;
+    c.err = misc + 128;
+    c.stats = (unsigned long long *)(misc + 192);
+    c.tw = tw;
+    c.th = th;
+    c.ntw = (int)ntw;
+    c.nth = (int)nth;
+    c.spin_ms = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
+    int rc = HCLIB_HIP_OK;
+    auto fail = [&](int r) { (void)hipFree(d); return r; };
+    if ((rc = hip_check(hipMemcpyAsync((void *)c.s1, s1, b_s1, hipMemcpyHostToDevice, m.stream), "copy s1"))) return fail(rc);
+    if ((rc = hip_check(hipMemcpyAsync((void *)c.s2, s2, b_s2, hipMemcpyHostToDevice, m.stream), "copy s2"))) return fail(rc);
+    if ((rc = hip_check(hipMemsetAsync(misc, 0, 1024, m.stream), "memset"))) return fail(rc);
+    {
+        uint32_t one = 1;  // tile 0 already sits at ready[0]
+        if ((rc = hip_check(hipMemcpyAsync(c.ready_tail, &one, 4, hipMemcpyHostToDevice, m.stream), "tail"))) return fail(rc);
+    }
+    hipLaunchKernelGGL(k_sw_init, dim3(1024), dim3(256), 0, m.stream, c.deps, c.ready, c.ntw, c.nth);
+    const size_t lds = 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + (size_t)tw + 16;
+    if (lds > 160 * 1024) return fail((set_error("hclib_hip_sw: tile width too large for LDS"), HCLIB_HIP_EINVAL));
+    int per_cu = (int)((160 * 1024) / lds);
+    int wpc = env_int("HCLIB_HIP_SW_WAVES_PER_CU", 8);
+    if (wpc > per_cu) wpc = per_cu;
+    if (wpc < 1) wpc = 1;
+    const int grid = m.num_cus * wpc;
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute((const void *)k_sw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if ((rc = hip_check(hipEventRecord(m.ev0, m.stream), "event"))) return fail(rc);
+    hipLaunchKernelGGL(k_sw, dim3(grid), dim3(64), lds, m.stream, c);
+    if ((rc = hip_check(hipGetLastError(), "k_sw launch"))) return fail(rc);
+    if ((rc = hip_check(hipEventRecord(m.ev1, m.stream), "event"))) return fail(rc);
+    uint32_t herr = 0;
+    unsigned long long st[2] = {0, 0};
+    int corner = 0;
+    if ((rc = hip_check(hipStreamSynchronize(m.stream), "k_sw"))) return fail(rc);
+    (void)hipMemcpy(&herr, c.err, 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(st, c.stats, 16, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&corner, c.corner + (nt - 1), 4, hipMemcpyDeviceToHost);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
+    (void)hipFree(d);
+    if (herr) {
+        set_error("hclib_hip_sw: device error %u", herr);
+        return HCLIB_HIP_EDEVICE;
+    }
+    if (st[0] != nt) {
+        set_error("hclib_hip_sw: executed %llu of %zu tiles", st[0], nt);
+        return HCLIB_HIP_EDEVICE;
+    }
+    *score = corner;  // bottom_row[tw-1] of the last tile == its corner (:239)
+    if (result) {
+        result->tiles = st[0];
+        result->releases = st[1];
+        result->kernel_ms = ms;
+        result->cells_per_s = (double)nt * tw * th / (ms * 1e-3);
+    }
+    return HCLIB_HIP_OK;
+}

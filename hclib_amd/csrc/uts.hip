@@ -1,0 +1,473 @@
+// uts.hip — UTS tree search as a device task kind of the megakernel.
+//
+// One lane-item = one rng_spawn (test/uts/rng/brg_sha1.c:68-83): the child
+// state is a single SHA-1 block compression of parent[20] || i, computed in
+// registers. A task entry is a non-leaf node with children left to spawn
+// (leaves are counted and never stored). numChildren (test/uts/uts.c:225-274)
+// runs on integer threshold tables that the host derives from the
+// reference's own libm formula (uts.c:171-222), so the device needs no libm
+// and stays bit-exact: n = #{k in 1..100 : thr[depth][k] <= rand}.
+// Counting follows UTS.cpp: a node counts when it is generated (each node is
+// popped exactly once in the reference), leaves when numChildren <= 0,
+// depth = max height.
+#include <math.h>
+#include <string.h>
+
+#include <vector>
+
+#include "hx_module.h"
+
+namespace hx {
+
+// ------------------------------------------------------------- SHA-1
+#define HX_ROTL(x, n) (((x) << (n)) | ((x) >> (32 - (n))))
+#define HX_RND(f, k, wi)                                \
+    {                                                   \
+        uint32_t t_ = HX_ROTL(a, 5) + (f) + e + (k) + (wi); \
+        e = d;                                          \
+        d = c;                                          \
+        c = HX_ROTL(b, 30);                             \
+        b = a;                                          \
+        a = t_;                                         \
+    }
+#define HX_F1 (d ^ (b & (c ^ d)))
+#define HX_F2 (b ^ c ^ d)
+#define HX_F3 ((b & c) | (d & (b ^ c)))
+#define HX_W(i) \
+    (w[(i) & 15] = HX_ROTL(w[((i) + 13) & 15] ^ w[((i) + 8) & 15] ^ w[((i) + 2) & 15] ^ w[(i) & 15], 1))
+
+// SHA-1 of the 16-word block w (destroyed), from the standard IV.
+__device__ __forceinline__ void sha1_block(uint32_t w[16], uint32_t h[5]) {
+    uint32_t a = 0x67452301u, b = 0xefcdab89u, c = 0x98badcfeu, d = 0x10325476u, e = 0xc3d2e1f0u;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) HX_RND(HX_F1, 0x5a827999u, w[i]);
+#pragma unroll
+    for (int i = 16; i < 20; ++i) HX_RND(HX_F1, 0x5a827999u, HX_W(i));
+#pragma unroll
+    for (int i = 20; i < 40; ++i) HX_RND(HX_F2, 0x6ed9eba1u, HX_W(i));
+#pragma unroll
+    for (int i = 40; i < 60; ++i) HX_RND(HX_F3, 0x8f1bbcdcu, HX_W(i));
+#pragma unroll
+    for (int i = 60; i < 80; ++i) HX_RND(HX_F2, 0xca62c1d6u, HX_W(i));
+    h[0] = 0x67452301u + a;
+    h[1] = 0xefcdab89u + b;
+    h[2] = 0x98badcfeu + c;
+    h[3] = 0x10325476u + d;
+    h[4] = 0xc3d2e1f0u + e;
+}
+
+// rng_spawn: SHA1(parent || i) with the 24-byte message padding.
+__device__ __forceinline__ void rng_spawn_dev(const uint32_t p[5], uint32_t i, uint32_t out[5]) {
+    uint32_t w[16];
+    w[0] = p[0];
+    w[1] = p[1];
+    w[2] = p[2];
+    w[3] = p[3];
+    w[4] = p[4];
+    w[5] = i;
+    w[6] = 0x80000000u;
+#pragma unroll
+    for (int k = 7; k < 15; ++k) w[k] = 0;
+    w[15] = 192;
+    sha1_block(w, out);
+}
+
+// --------------------------------------------------------- depth rules
+// rule.x: 0 = constant rule.y children; 1 = BIN: rand < rule.y ? m : 0;
+//         2 = GEO: threshold table rule.z (128 words, entries 1..100)
+struct UtsCtx {
+    uint32_t root[5];
+    int root_nc;
+    int nrules;
+    int stationary;
+    int gran;
+    int m;
+    int shard, nshards, split;
+    int hist_levels;
+    const int4 *rules;
+    const uint32_t *thr;
+    unsigned long long *hist;
+};
+
+__device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32_t *err) {
+    int ri = d;
+    if (d >= c.nrules) {
+        if (!c.stationary) {
+            dev_error(err, kErrDepthTable);
+            return 0;
+        }
+        ri = c.nrules - 1;
+    }
+    const int4 rule = c.rules[ri];
+    if (rule.x == 0) return rule.y;
+    if (rule.x == 1) return r < (uint32_t)rule.y ? c.m : 0;
+    const uint32_t *t = c.thr + (size_t)rule.z * 128;
+    int lo = 0, hi = 100;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+        int mid = (lo + hi + 1) >> 1;
+        if (lo < hi) {
+            if (t[mid] <= r) lo = mid;
+            else hi = mid - 1;
+        }
+    }
+    return lo;
+}
+
+struct UtsKind {
+    static constexpr int kWords = 8;  // st[5], height, nchild, start
+    static constexpr int kMaxOut = 1;
+    using Ctx = UtsCtx;
+    struct Acc {
+        unsigned long long nodes = 0, leaves = 0;
+        uint32_t maxd = 0;
+        __device__ void flush(SchedGlobals *g) {
+            unsigned long long n = wave_sum(nodes), l = wave_sum(leaves);
+            uint32_t m = wave_max(maxd);
+            if (lane_id() == 0) {
+                add_agent(&g->counters[0], n);
+                add_agent(&g->counters[1], l);
+                __hip_atomic_fetch_max(&g->maxes[0], (unsigned long long)m, __ATOMIC_RELAXED, HX_AGENT);
+            }
+        }
+    };
+    __device__ static uint32_t count(const uint32_t *e) { return e[6]; }
+
+    __device__ static int roots(const Ctx &c, Acc &acc, uint32_t (*out)[kWords]) {
+        // the root node (height 0) is counted once, by shard 0
+        if (lane_id() == 0 && c.shard == 0) {
+            acc.nodes += 1;
+            if (c.root_nc <= 0) acc.leaves += 1;
+            if (c.hist && c.hist_levels > 0) atomicAdd(&c.hist[0], 1ull);
+        }
+        if (c.root_nc <= 0) return 0;
+        for (int k = 0; k < 5; ++k) out[0][k] = c.root[k];
+        out[0][5] = 0;
+        out[0][6] = (uint32_t)c.root_nc;
+        out[0][7] = 0;
+        return 1;
+    }
+
+    __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *e, uint32_t k,
+                                  uint32_t (*out)[kWords], uint32_t *err) {
+        uint32_t ch[5];
+        rng_spawn_dev(e, k, ch);
+        for (int g = 1; g < c.gran; ++g) rng_spawn_dev(e, k, ch);  // -g: repeated spawns
+        const int h1 = (int)e[5] + 1;
+        bool counted = true;
+        if (c.nshards > 1) {
+            if (h1 == c.split && (ch[0] % (uint32_t)c.nshards) != (uint32_t)c.shard) return 0;
+            if (h1 < c.split && c.shard != 0) counted = false;
+        }
+        const int nc = uts_nc(c, h1, ch[4] & 0x7fffffffu, err);
+        if (counted) {
+            acc.nodes += 1;
+            if (nc <= 0) acc.leaves += 1;
+            acc.maxd = acc.maxd > (uint32_t)h1 ? acc.maxd : (uint32_t)h1;
+            if (c.hist && h1 < c.hist_levels) atomicAdd(&c.hist[h1], 1ull);
+        }
+        if (nc <= 0) return 0;
+        out[0][0] = ch[0];
+        out[0][1] = ch[1];
+        out[0][2] = ch[2];
+        out[0][3] = ch[3];
+        out[0][4] = ch[4];
+        out[0][5] = (uint32_t)h1;
+        out[0][6] = (uint32_t)nc;
+        out[0][7] = 0;
+        return 1;
+    }
+};
+
+constexpr int kUtsCap = 512;
+
+__global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, SchedGlobals *g,
+                                                   SchedConfig cfg) {
+    __shared__ WaveStack<UtsKind, kUtsCap> st;
+    run_worker<UtsKind, kUtsCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
+}
+
+// ------------------------------------------------------ host: rules/tables
+// The reference's per-node formula, uts.c:143-222, evaluated with libm.
+static int cvt_int_x86(double x) {
+    // (int) conversion as x86-64 cvttsd2si: NaN / out of range -> INT_MIN
+    if (!(x >= -2147483648.0 && x < 2147483648.0)) return (int)0x80000000u;
+    return (int)x;
+}
+
+static double geo_bi(const hclib_hip_uts_params_t &p, int depth) {
+    double b_i = p.b_0;
+    if (depth > 0) {
+        switch (p.shape_fn) {
+        case 1: b_i = p.b_0 * pow((double)depth, -log(p.b_0) / log((double)p.gen_mx)); break;
+        case 2:
+            if (depth > 5 * p.gen_mx) { b_i = 0.0; break; }
+            b_i = pow(p.b_0, sin(2.0 * 3.141592653589793 * (double)depth / (double)p.gen_mx));
+            break;
+        case 3: b_i = (depth < p.gen_mx) ? p.b_0 : 0; break;
+        default: b_i = p.b_0 * (1.0 - (double)depth / (double)p.gen_mx); break;
+        }
+    }
+    return b_i;
+}
+
+static int geo_n(double prob, uint32_t h) {
+    double u = (double)(int)h / 2147483648.0;
+    return cvt_int_x86(floor(log(1 - u) / log(1 - prob)));
+}
+
+struct UtsTables {
+    std::vector<int4> rules;
+    std::vector<uint32_t> thr;  // 128 words per geo table
+    int stationary = 1;
+    int root_nc = 0;
+    uint32_t root[5];
+};
+
+static void sha1_host(uint32_t w[16], uint32_t h[5]) {
+    uint32_t a = 0x67452301u, b = 0xefcdab89u, c = 0x98badcfeu, d = 0x10325476u, e = 0xc3d2e1f0u;
+    for (int i = 0; i < 80; ++i) {
+        uint32_t wi = (i < 16) ? w[i] : HX_W(i);
+        if (i < 20) HX_RND(HX_F1, 0x5a827999u, wi)
+        else if (i < 40) HX_RND(HX_F2, 0x6ed9eba1u, wi)
+        else if (i < 60) HX_RND(HX_F3, 0x8f1bbcdcu, wi)
+        else HX_RND(HX_F2, 0xca62c1d6u, wi)
+    }
+    h[0] = 0x67452301u + a;
+    h[1] = 0xefcdab89u + b;
+    h[2] = 0x98badcfeu + c;
+    h[3] = 0x10325476u + d;
+    h[4] = 0xc3d2e1f0u + e;
+}
+
+// Build the geo table for b_i; returns table index (deduplicated) or -1 for
+// "always 0 children"; -2 if the formula is not monotone in rand (unsupported).
+static int geo_table(UtsTables &T, double b_i) {
+    const double prob = 1.0 / (1.0 + b_i);
+    uint32_t thr[128];
+    thr[0] = 0;
+    bool any = false;
+    const int nmax = geo_n(prob, 0x7fffffffu);
+    for (int k = 1; k <= 100; ++k) {
+        if (nmax < k) {  // never reached (INT_MIN / capped by the range end)
+            thr[k] = 0x80000000u;
+            continue;
+        }
+        uint32_t lo = 0, hi = 0x7fffffffu;  // smallest h with n(h) >= k
+        while (lo < hi) {
+            uint32_t mid = lo + (hi - lo) / 2;
+            if (geo_n(prob, mid) >= k) hi = mid;
+            else lo = mid + 1;
+        }
+        thr[k] = lo;
+        any = true;
+    }
+    for (int k = 101; k < 128; ++k) thr[k] = 0x80000000u;
+    if (!any) return -1;
+    // spot-verify monotonicity / table agreement around every threshold
+    for (int k = 1; k <= 100; ++k) {
+        if (thr[k] == 0x80000000u) break;
+        for (int dlt = -2; dlt <= 2; ++dlt) {
+            int64_t hh = (int64_t)thr[k] + dlt;
+            if (hh < 0 || hh > 0x7fffffff) continue;
+            int n = geo_n(prob, (uint32_t)hh);
+            int want = n < 0 ? 0 : (n > 100 ? 100 : n);
+            int got = 0;
+            for (int q = 1; q <= 100; ++q) got += thr[q] <= (uint32_t)hh;
+            if (got != want) return -2;
+        }
+    }
+    const size_t nt = T.thr.size() / 128;
+    if (nt && !memcmp(&T.thr[(nt - 1) * 128], thr, sizeof(thr))) return (int)(nt - 1);
+    T.thr.insert(T.thr.end(), thr, thr + 128);
+    return (int)nt;
+}
+
+static int bin_threshold(double q) {
+    // smallest h with h/2^31 >= q; rand < thr  <=>  d < q (uts.c:162-168)
+    uint32_t lo = 0, hi = 0x80000000u;
+    while (lo < hi) {
+        uint32_t mid = lo + (hi - lo) / 2;
+        if (((double)(int)mid) / 2147483648.0 >= q) hi = mid;
+        else lo = mid + 1;
+    }
+    return (int)lo;
+}
+
+static int build_tables(const hclib_hip_uts_params_t &p, UtsTables &T) {
+    T.rules.clear();
+    T.thr.clear();
+    auto geo_rule = [&](int d) -> int4 {
+        int t = geo_table(T, geo_bi(p, d));
+        if (t == -1) return make_int4(0, 0, 0, 0);
+        if (t == -2) return make_int4(-1, 0, 0, 0);
+        return make_int4(2, 0, t, 0);
+    };
+    int D = 0;
+    switch (p.type) {
+    case 0:  // BIN
+        T.rules.push_back(make_int4(0, 0, 0, 0));  // root handled by root_nc
+        T.rules.push_back(make_int4(1, bin_threshold(p.non_leaf_prob), 0, 0));
+        T.stationary = 1;
+        break;
+    case 1:  // GEO
+        if (p.shape_fn == 3 || p.shape_fn == 0) { D = p.gen_mx + 1; T.stationary = 1; }
+        else if (p.shape_fn == 2) { D = 5 * p.gen_mx + 2; T.stationary = 1; }
+        else { D = 4096; T.stationary = 0; }
+        for (int d = 0; d < D; ++d) T.rules.push_back(geo_rule(d));
+        if (T.stationary) T.rules.push_back(make_int4(0, 0, 0, 0));
+        break;
+    case 2: {  // HYBRID: geo below shift_depth*gen_mx, bin after
+        int d = 0;
+        for (; d < p.shift_depth * p.gen_mx; ++d) T.rules.push_back(geo_rule(d));
+        T.rules.push_back(make_int4(1, bin_threshold(p.non_leaf_prob), 0, 0));
+        T.stationary = 1;
+        break;
+    }
+    case 3:  // BALANCED
+        for (int d = 0; d < p.gen_mx; ++d) T.rules.push_back(make_int4(0, (int)p.b_0, 0, 0));
+        T.rules.push_back(make_int4(0, 0, 0, 0));
+        T.stationary = 1;
+        break;
+    default:
+        set_error("uts: unknown tree type %d", p.type);
+        return HCLIB_HIP_EINVAL;
+    }
+    for (auto &r : T.rules)
+        if (r.x == -1) {
+            set_error("uts: numChildren is not monotone in rand for these parameters");
+            return HCLIB_HIP_EINVAL;
+        }
+    if (T.thr.empty()) T.thr.assign(128, 0x80000000u);
+    // the root (uts_initRoot uts.c:151-159 + uts_numChildren at height 0)
+    uint32_t w[16] = {0};
+    w[4] = (uint32_t)p.root_id;
+    w[5] = 0x80000000u;
+    w[15] = 160;
+    sha1_host(w, T.root);
+    const uint32_t r = T.root[4] & 0x7fffffffu;
+    int nc = 0;
+    switch (p.type) {
+    case 0: nc = (int)floor(p.b_0); break;
+    case 1: nc = geo_n(1.0 / (1.0 + geo_bi(p, 0)), r); break;
+    case 2: nc = (0 < p.shift_depth * p.gen_mx) ? geo_n(1.0 / (1.0 + geo_bi(p, 0)), r)
+                                               : ((((double)(int)r) / 2147483648.0 < p.non_leaf_prob) ? p.non_leaf_bf : 0);
+            break;
+    case 3: nc = (0 < p.gen_mx) ? (int)p.b_0 : 0; break;
+    }
+    if (p.type == 0) {
+        int root_bf = (int)ceil(p.b_0);
+        if (nc > root_bf) nc = root_bf;
+    } else if (p.type != 3 && nc > 100) {
+        nc = 100;
+    }
+    T.root_nc = nc;
+    return HCLIB_HIP_OK;
+}
+
+static int host_nc(const hclib_hip_uts_params_t &p, const UtsTables &T, int d, uint32_t r) {
+    int ri = d < (int)T.rules.size() ? d : (int)T.rules.size() - 1;
+    int4 rule = T.rules[ri];
+    if (rule.x == 0) return rule.y;
+    if (rule.x == 1) return r < (uint32_t)rule.y ? p.non_leaf_bf : 0;
+    int n = 0;
+    for (int k = 1; k <= 100; ++k) n += T.thr[(size_t)rule.z * 128 + k] <= r;
+    return n;
+}
+
+}  // namespace hx
+
+using namespace hx;
+
+extern "C" int hclib_hip_uts_num_children_host(const hclib_hip_uts_params_t *params, int height,
+                                               const uint32_t st[5]) {
+    // tables are pure functions of the parameters: cache the last set
+    static hclib_hip_uts_params_t last_p;
+    static UtsTables T;
+    static bool have = false;
+    if (!have || memcmp(&last_p, params, sizeof(last_p)) != 0) {
+        have = false;
+        if (build_tables(*params, T) != HCLIB_HIP_OK) return -1;
+        last_p = *params;
+        have = true;
+    }
+    if (height == 0) return T.root_nc;
+    return host_nc(*params, T, height, st[4] & 0x7fffffffu);
+}
+
+extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int shard, int nshards,
+                                    int split_depth, hclib_hip_uts_result_t *result,
+                                    uint64_t *level_hist, int max_levels) {
+    if (!params || !result || nshards < 1 || shard < 0 || shard >= nshards || max_levels < 0 ||
+        max_levels > 1024 || (nshards > 1 && split_depth < 1)) {
+        set_error("hclib_hip_uts_search: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    Module &m = mod();
+    UtsTables T;
+    HX_TRY(build_tables(*params, T));
+
+    // device copies of the rule tables (+ optional histogram)
+    const size_t rb = T.rules.size() * sizeof(int4), tb = T.thr.size() * 4,
+                 hb = (size_t)max_levels * 8;
+    void *dmem = nullptr;
+    HX_HIP(hipMalloc(&dmem, rb + tb + hb + 512));
+    char *dp = (char *)dmem;
+    int4 *d_rules = (int4 *)dp;
+    uint32_t *d_thr = (uint32_t *)(dp + ((rb + 255) & ~(size_t)255));
+    unsigned long long *d_hist =
+        (unsigned long long *)(dp + ((rb + 255) & ~(size_t)255) + ((tb + 255) & ~(size_t)255));
+    HX_HIP(hipMemcpyAsync(d_rules, T.rules.data(), rb, hipMemcpyHostToDevice, m.stream));
+    HX_HIP(hipMemcpyAsync(d_thr, T.thr.data(), tb, hipMemcpyHostToDevice, m.stream));
+    if (max_levels) HX_HIP(hipMemsetAsync(d_hist, 0, hb, m.stream));
+
+    UtsCtx ctx;
+    memcpy(ctx.root, T.root, sizeof(ctx.root));
+    ctx.root_nc = T.root_nc;
+    ctx.nrules = (int)T.rules.size();
+    ctx.stationary = T.stationary;
+    ctx.gran = params->compute_gran < 1 ? 1 : params->compute_gran;
+    ctx.m = params->non_leaf_bf;
+    ctx.shard = shard;
+    ctx.nshards = nshards;
+    ctx.split = split_depth;
+    ctx.hist_levels = max_levels;
+    ctx.rules = d_rules;
+    ctx.thr = d_thr;
+    ctx.hist = max_levels ? d_hist : nullptr;
+
+    PoolView pool;
+    const uint32_t nq = (uint32_t)env_int("HCLIB_HIP_DEQUES", 64);
+    HX_TRY(make_pool(nq, (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
+                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 32), UtsKind::kWords, &pool));
+    SchedConfig cfg;
+    cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_SPILL_HI", 320);
+    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", 32);
+    cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
+    HX_TRY(reset_sched(pool, 1));
+    const int grid = m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 8);
+    HX_HIP(hipEventRecord(m.ev0, m.stream));
+    hipLaunchKernelGGL(k_uts_search, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
+    HX_HIP(hipGetLastError());
+    HX_HIP(hipEventRecord(m.ev1, m.stream));
+    SchedGlobals gl;
+    int rc = finish_sched(&gl, "hclib_hip_uts_search");
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
+    if (rc == HCLIB_HIP_OK && max_levels) {
+        std::vector<unsigned long long> h(max_levels);
+        HX_HIP(hipMemcpy(h.data(), d_hist, hb, hipMemcpyDeviceToHost));
+        for (int i = 0; i < max_levels; ++i) level_hist[i] = h[i];
+    }
+    (void)hipFree(dmem);
+    if (rc != HCLIB_HIP_OK) return rc;
+    result->nodes = gl.counters[0];
+    result->leaves = gl.counters[1];
+    result->max_depth = gl.maxes[0];
+    result->batches = gl.counters[13];
+    result->chunks_pushed = gl.counters[14];
+    result->chunks_stolen = gl.counters[15];
+    result->kernel_ms = ms;
+    return HCLIB_HIP_OK;
+}

@@ -1,0 +1,200 @@
+/*
+ * hclib_hip.h — the MI355X `modules/hip` C ABI.
+ *
+ * HClib's plug-in ABI lets a module add a locale type and run work there
+ * (inc/hclib-module.h:62-106, src/hclib_module.c:49-160). The reference's
+ * only device module, modules/cuda, runs kernels from CPU tasks and polls
+ * for completion (modules/cuda/inc/hclib_cuda.h:21-74). This module instead
+ * moves the scheduler itself onto the GPU: every entry point below replaces
+ * a piece of the reference's CPU hot path with a hand-written gfx950 kernel.
+ *
+ *   entry point                      replaces (reference file:line)
+ *   -------------------------------  -------------------------------------------
+ *   hclib_hip_forasync1d/2d/3d       hclib_forasync + forasync{1,2,3}D_{flat,
+ *                                    recursive,runner}  src/hclib.c:110-464
+ *   hclib_hip_forasync_triad_f32     the forasync1D_runner loop of a triad body
+ *                                    src/hclib.c:110-120 (BASELINE config 1)
+ *   hclib_hip_uts_search             core_work_loop/find_and_run_task/deque_*
+ *                                    src/hclib-runtime.c:646-729,
+ *                                    src/hclib-deque.c:50-139, driving the UTS
+ *                                    tasks of test/uts/UTS.cpp:154-232
+ *   hclib_hip_fib                    spawn/finish counters of test/fib/fib.c:57-71
+ *                                    (async/finish) and 113-141 (DDT), i.e.
+ *                                    src/hclib-runtime.c:431-446, 572-617,
+ *                                    1219-1277
+ *   hclib_hip_sw                     promise put / waiter release of
+ *                                    src/hclib-promise.c:132-245 driving the tile
+ *                                    DAG of test/smithwaterman/smith_waterman.cpp
+ *                                    :119-239
+ *   hclib_hip_dag_*                  the same dependency-counter release for any
+ *                                    async_await DAG built through hclib.h
+ *
+ * Conventions (mirroring the reference's error behaviour):
+ * plain pointers and sizes only; functions return 0 on success and a
+ * negative HCLIB_HIP_E* code on failure, with a message retrievable via
+ * hclib_hip_last_error(). Device-side failures (queue overflow, bounded
+ * spins that time out) set a device error word that the host checks after
+ * every launch. Nothing here ever falls back to the CPU: without a usable
+ * gfx950 device every compute entry point fails with HCLIB_HIP_ENODEV.
+ */
+#ifndef HCLIB_HIP_H_
+#define HCLIB_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HCLIB_HIP_OK 0
+#define HCLIB_HIP_ENODEV (-1)   /* no HIP device / not gfx950 */
+#define HCLIB_HIP_EINVAL (-2)   /* bad arguments */
+#define HCLIB_HIP_ENOMEM (-3)   /* device allocation failed */
+#define HCLIB_HIP_EDEVICE (-4)  /* device-side error word set (see message) */
+#define HCLIB_HIP_EHIP (-5)     /* a HIP runtime call failed */
+
+/* ---------------------------------------------------------------- module */
+/* hclib_hip_init: bind the calling process to HIP device `device` (the
+ * module's post-init hook, inc/hclib-module.h:62-64). Idempotent. */
+int hclib_hip_init(int device);
+void hclib_hip_finalize(void);
+const char *hclib_hip_last_error(void);
+/* Number of CUs / XCDs of the bound device (0 if none). */
+int hclib_hip_num_cus(void);
+/* Module version string, also proves the library loads without a GPU. */
+const char *hclib_hip_version(void);
+
+/* ------------------------------------------------------------ forasync */
+/* hclib_loop_domain_t of inc/hclib-task.h:53-58 (int bounds, 16 bytes). */
+typedef struct {
+    int low;
+    int high;
+    int stride;
+    int tile;
+} hclib_hip_loop_domain_t;
+
+#define HCLIB_HIP_FORASYNC_FLAT 0      /* FORASYNC_MODE_FLAT, inc/hclib.h:161 */
+#define HCLIB_HIP_FORASYNC_RECURSIVE 1 /* FORASYNC_MODE_RECURSIVE, inc/hclib.h:159 */
+
+/* Device loop bodies. A host function pointer cannot run on the GPU, so a
+ * forasync at the GPU locale names one of these registered body kinds. */
+#define HCLIB_HIP_BODY_TRIAD_F32 1 /* a[i] = b[i] + s*c[i] (1-D) */
+#define HCLIB_HIP_BODY_IOTA_CHECK 2 /* assert(ran[i]==-1); ran[i]=i, as test/c/forasync1DCh.c:45-49 (1-D) */
+#define HCLIB_HIP_BODY_VISIT_COUNT 3 /* counts[linear(i,j,k)] += 1 (1/2/3-D) */
+
+typedef struct {
+    float *a;
+    const float *b;
+    const float *c;
+    float s;
+} hclib_hip_triad_args_t;
+
+typedef struct {
+    int *ran;      /* device pointer, indexed by i */
+    int *errors;   /* device pointer to one int: number of failed checks */
+} hclib_hip_iota_args_t;
+
+typedef struct {
+    int *counts;   /* device pointer */
+    int base[3];   /* index origin per dim */
+    int extent[3]; /* counts has extent[0]*extent[1]*extent[2] ints, row-major */
+} hclib_hip_visit_args_t;
+
+/* hclib_forasync (src/hclib.c:452-464) for dim in 1..3 at the GPU locale.
+ * `domain` has `dim` entries; tile == -1 is replaced by
+ * ceil((high-low)/nworkers) with nworkers = the module's worker count (the
+ * number of resident waves, hclib_hip_num_workers()) and written back, as
+ * the reference does. The iteration set is exactly the reference's for the
+ * given mode (including the FLAT 1-D quirk of src/hclib.c:322-337).
+ * `args` points to the body's argument struct (host memory, copied by
+ * value). `stream` is a hipStream_t (NULL = default). Asynchronous: the
+ * call returns after enqueueing; synchronize on the stream. */
+int hclib_hip_forasync(int body, const void *args, int dim, hclib_hip_loop_domain_t *domain,
+                       int mode, void *stream);
+
+/* Fast path of hclib_hip_forasync for the triad over [0, n): coalesced
+ * grid-stride float4 tiles, no FMA contraction (bit-exact with the CPU). */
+int hclib_hip_forasync_triad_f32(float *a, const float *b, const float *c, float s, int64_t n,
+                                 void *stream);
+
+/* Resident worker waves the forasync/megakernel launches use. */
+int hclib_hip_num_workers(void);
+
+/* ----------------------------------------------------------------- UTS */
+/* Tree parameters: the UTS CLI flags of test/uts/uts.c:380-420 (same field
+ * order as oracle/uts_oracle.h so both sides read the same struct). */
+typedef struct {
+    int type;         /* -t: 0 BIN, 1 GEO, 2 HYBRID, 3 BALANCED */
+    int shape_fn;     /* -a: 0 LINEAR, 1 EXPDEC, 2 CYCLIC, 3 FIXED */
+    int gen_mx;       /* -d */
+    int root_id;      /* -r */
+    int non_leaf_bf;  /* -m */
+    int compute_gran; /* -g */
+    double b_0;       /* -b */
+    double non_leaf_prob; /* -q */
+    double shift_depth;   /* -f */
+} hclib_hip_uts_params_t;
+
+typedef struct {
+    uint64_t nodes;     /* tree size   (UTS.cpp:241, uts.c:462) */
+    uint64_t leaves;    /* num leaves */
+    uint64_t max_depth; /* tree depth */
+    uint64_t chunks_pushed;  /* work chunks spilled to the HBM deques */
+    uint64_t chunks_stolen;  /* chunks taken from another worker's deque */
+    uint64_t batches;        /* wave batches executed */
+    double kernel_ms;        /* device time of the search launch (HIP events) */
+} hclib_hip_uts_result_t;
+
+/* Search the whole tree on the bound GPU (persistent megakernel: per-wave
+ * LDS stacks, per-XCD chunk deques in HBM, device-atomic stealing,
+ * outstanding-work termination). Multi-GPU sharding: with nshards > 1 the
+ * top of the tree is expanded identically on every shard until the
+ * frontier holds >= min_frontier nodes; shard `shard` then searches the
+ * frontier nodes whose index is congruent to shard (mod nshards) and counts
+ * the expanded top nodes only when shard == 0. Per-shard results sum to
+ * the whole tree (max for depth). level_hist (host, may be NULL) receives
+ * nodes per depth for depth < max_levels (max_levels <= 1024). */
+int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int shard, int nshards,
+                         int min_frontier, hclib_hip_uts_result_t *result, uint64_t *level_hist,
+                         int max_levels);
+
+/* Host-side helper (no GPU needed): evaluate the integer numChildren rule
+ * the device uses (threshold tables built from the reference's libm
+ * formula, uts.c:171-274) for an explicit node; lets the CPU tests check
+ * the tables against the oracle. st = the 5 big-endian state words. */
+int hclib_hip_uts_num_children_host(const hclib_hip_uts_params_t *params, int height,
+                                    const uint32_t st[5]);
+
+/* ----------------------------------------------------------------- fib */
+typedef struct {
+    uint64_t tasks;      /* fib tasks executed (each fib(n) call is one task) */
+    uint64_t joins;      /* finish scopes closed (join counters reaching 0) */
+    uint64_t chunks_pushed;
+    uint64_t chunks_stolen;
+    double kernel_ms;
+} hclib_hip_fib_result_t;
+
+/* fib(n) with one task per call and a join counter per finish scope
+ * (continuation by the last arriver). n <= 80. */
+int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *result);
+
+/* ---------------------------------------------------------------- SW */
+typedef struct {
+    uint64_t tiles;      /* tile tasks executed */
+    uint64_t releases;   /* dependency-counter decrements */
+    double kernel_ms;
+    double cells_per_s;
+} hclib_hip_sw_result_t;
+
+/* Tiled global alignment of smith_waterman.cpp over host sequences coded
+ * 1..4 (A,C,G,T). Tile grid = (n1/tw) x (n2/th); remainders dropped as the
+ * reference does. tw must be a multiple of 64... no: any tw <= 4096, th a
+ * multiple of 64 or th <= 64*16. Writes the score (bottom-right cell). */
+int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_t n2, int tw, int th,
+                 int *score, hclib_hip_sw_result_t *result);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HCLIB_HIP_H_ */

@@ -178,3 +178,49 @@ def forasync1d_counts(low, high, stride, tile, mode, nworkers, base, ncounts):
         low, high, stride, tile, mode, nworkers, base,
         counts.ctypes.data_as(C.POINTER(C.c_int32)), ncounts)
     return tile_used, counts
+
+
+def forasync_nd_counts(domains, mode, nworkers, bases, extents):
+    """Visit counts of hclib_forasync for dim 1..3 (src/hclib.c:110-464):
+    1-D uses the exact 1-D lowering (incl. the FLAT quirk); 2-D/3-D FLAT
+    tiles each dimension with clamped tiles (src/hclib.c:353-416), RECURSIVE
+    bisects each dimension (192-314); the runner restarts the stride at every
+    tile's low bound. Returns (tiles_used, counts ndarray)."""
+    import numpy as np
+
+    dom = [list(d) for d in domains]
+    for d in dom:
+        if d[3] == -1:
+            d[3] = ((d[1] - d[0]) + nworkers - 1) // nworkers
+    if len(dom) == 1:
+        t, c = forasync1d_counts(*dom[0], mode, nworkers, bases[0], extents[0])
+        return [t], c
+
+    def per_dim(low, high, stride, tile):
+        idx = []
+        if mode == 1:
+            def rec(lo, hi):
+                if hi - lo > tile:
+                    mid = (hi + lo) // 2
+                    rec(lo, mid)
+                    rec(mid, hi)
+                else:
+                    idx.extend(range(lo, hi, stride))
+            rec(low, high)
+        else:
+            lo = low
+            while lo < high:
+                hi = min(lo + tile, high)
+                idx.extend(range(lo, hi, stride))
+                lo += tile
+        return idx
+
+    sets = [per_dim(*d) for d in dom]
+    counts = np.zeros(extents, dtype=np.int32)
+    import itertools
+
+    for tup in itertools.product(*sets):
+        loc = tuple(v - b for v, b in zip(tup, bases))
+        if all(0 <= l < e for l, e in zip(loc, extents)):
+            counts[loc] += 1
+    return [d[3] for d in dom], counts

@@ -1,0 +1,101 @@
+"""CPU-side checks of the product's C ABI: the library builds for gfx950,
+loads without a GPU, exports every declared symbol, and its host-side UTS
+threshold tables agree with the reference's numChildren vectors.
+No compute call runs here."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import hclib_amd as H
+from tests.conftest import ROOT
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(hclib_\w+)\s*\(", txt)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = H.lib()
+    for header in ("hclib_hip.h", "hclib.h"):
+        path = os.path.join(ROOT, "include", header)
+        if not os.path.exists(path):
+            continue
+        for sym in _declared(header):
+            assert hasattr(lib, sym), f"{sym} declared in {header} but not exported"
+    for sym in H.EXPORTS_HIP:
+        assert hasattr(lib, sym)
+    assert "gfx950" in H.version()
+
+
+def test_built_for_gfx950_only():
+    out = os.popen(f"/opt/rocm/lib/llvm/bin/llvm-objdump --offloading {H.LIB_PATH} 2>/dev/null"
+                   f" | grep -o 'gfx[0-9a-z]*' | sort -u").read().split()
+    if not out:  # older objdump: fall back to the clang offload bundle marker
+        data = open(H.LIB_PATH, "rb").read()
+        out = sorted(set(m.decode() for m in re.findall(rb"gfx[0-9]{3}[a-z]?", data)))
+    assert out and set(out) == {"gfx950"}, out
+
+
+def _words(hexstr):
+    b = bytes.fromhex(hexstr)
+    return [int.from_bytes(b[4 * k:4 * k + 4], "big") for k in range(5)]
+
+
+@pytest.mark.parametrize("name", ["T1", "T2", "T3", "T4", "T5", "T3L"])
+def test_uts_device_tables_match_reference_vectors(golden, name):
+    g = golden("uts_goldens.json")
+    p = H.parse_uts_args(g["published"][name]["args"])
+    for st, h, nc in g["num_children"][name]:
+        if h == 0:
+            continue  # root rule is checked below
+        want = nc if nc > 0 else 0
+        got = H.uts_num_children_host(p, h, _words(st))
+        assert max(got, 0) == want, (name, st, h, got, nc)
+
+
+@pytest.mark.parametrize("name", ["T1", "T3", "T3L", "T5"])
+def test_uts_device_root_rule(golden, name):
+    from oracle import loader as L
+
+    g = golden("uts_goldens.json")
+    args = g["published"][name]["args"]
+    p = H.parse_uts_args(args)
+    op = L.parse_uts_args(args)
+    root = L.rng_init(op.root_id)
+    assert H.uts_num_children_host(p, 0, root) == L.uts_num_children(op, op.type, 0, root)
+
+
+def test_uts_tables_random_states_vs_oracle():
+    """Random spawn states at every depth of T1/T2/T4/T5 vs the libm oracle."""
+    import random
+
+    from oracle import loader as L
+
+    rng = random.Random(7)
+    for args in ["-t 1 -a 3 -d 10 -b 4 -r 19", "-t 1 -a 2 -d 16 -b 6 -r 502",
+                 "-t 2 -a 0 -d 16 -b 6 -r 1 -q 0.234375 -m 4 -r 1", "-t 1 -a 0 -d 20 -b 4 -r 34",
+                 "-t 1 -a 1 -d 8 -b 3 -r 5"]:
+        p = H.parse_uts_args(args)
+        op = L.parse_uts_args(args)
+        st = L.rng_init(op.root_id)
+        for k in range(3000):
+            st = L.rng_spawn(st, rng.randrange(100))
+            h = rng.randrange(1, 40)
+            want = max(0, L.uts_num_children(op, op.type, h, st))
+            assert max(0, H.uts_num_children_host(p, h, st)) == want, (args, h)
+
+
+def test_compute_entry_points_fail_loudly_without_gpu():
+    """No CPU fallback: without a gfx950 device the compute calls raise."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(H.HclibError):
+        H.fib(10)
+    with pytest.raises(H.HclibError):
+        H.uts("-t 1 -a 3 -d 10 -b 4 -r 19")

@@ -1,0 +1,243 @@
+"""GPU parity tests: every hot-path kernel, through the C ABI, against the
+CPU oracle (oracle/) and the reference's golden fixtures (tests/golden/).
+Bit-exact for all integer work; the fp32 triad is bit-exact too (no FMA
+contraction on either side), i.e. within the 1-ulp tolerance north_star
+allows with 0 ulp observed."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import hclib_amd as H  # noqa: E402
+from oracle import loader as L  # noqa: E402
+from tests.conftest import GOLD  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    H.init(0)
+    yield
+
+
+# ------------------------------------------------------------------ forasync
+def _triad_expected(b, c, s):
+    import torch
+
+    return torch.add(b, torch.mul(c, s))  # two rounded ops, no contraction
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 1000, 4097, 1 << 20, (1 << 20) + 7])
+def test_triad_small_bit_exact(n):
+    import torch
+
+    g = torch.Generator(device="cpu").manual_seed(n)
+    b = torch.rand(n, generator=g).cuda()
+    c = torch.rand(n, generator=g).cuda()
+    a = torch.full((n,), float("nan"), device="cuda")
+    s = 3.0
+    H.triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), s, n,
+                torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    exp = (b.cpu().numpy() + np.float32(s) * c.cpu().numpy()).astype(np.float32)
+    assert np.array_equal(a.cpu().numpy(), exp)
+
+
+def test_triad_full_size_2p28():
+    """BASELINE config 1 size: 2^28 fp32, s=3.0; checked element-wise on
+    device against two separately rounded torch ops."""
+    import torch
+
+    n = 1 << 28
+    g = torch.Generator(device="cuda").manual_seed(1)
+    b = torch.rand(n, device="cuda", generator=g)
+    c = torch.rand(n, device="cuda", generator=g)
+    a = torch.empty(n, device="cuda")
+    H.triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), 3.0, n,
+                torch.cuda.current_stream().cuda_stream)
+    exp = _triad_expected(b, c, 3.0)
+    assert torch.equal(a, exp)
+
+
+def test_triad_through_forasync_api():
+    import torch
+
+    n = 123457
+    b = torch.rand(n, device="cuda")
+    c = torch.rand(n, device="cuda")
+    a = torch.zeros(n, device="cuda")
+    args = H.TriadArgs(a.data_ptr(), b.data_ptr(), c.data_ptr(), 2.5)
+    for mode in (H.FORASYNC_MODE_FLAT, H.FORASYNC_MODE_RECURSIVE):
+        a.zero_()
+        dom = H.forasync(H.BODY_TRIAD_F32, args, [(0, n, 1, -1)], mode,
+                         torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert dom[0][3] == (n + H.num_workers() - 1) // H.num_workers()  # tile write-back
+        assert torch.equal(a, _triad_expected(b, c, 2.5))
+
+
+def test_forasync1d_iota_check():
+    """test/c/forasync1DCh.c: H1=1024, T1=33, FLAT; every ran[i]==-1 before."""
+    import torch
+
+    ran = torch.full((1024,), -1, dtype=torch.int32, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    H.forasync(H.BODY_IOTA_CHECK, H.IotaArgs(ran.data_ptr(), err.data_ptr()),
+               [(0, 1024, 1, 33)], H.FORASYNC_MODE_FLAT)
+    torch.cuda.synchronize()
+    assert err.item() == 0
+    assert torch.equal(ran.cpu(), torch.arange(1024, dtype=torch.int32))
+
+
+CASES_1D = [
+    ((10, 100, 1, 33), 0), ((10, 100, 1, 33), 1), ((0, 1000, 3, 7), 0), ((0, 1000, 3, 7), 1),
+    ((5, 777, 4, -1), 0), ((5, 777, 4, -1), 1), ((0, 0, 1, 5), 0), ((3, 4, 1, 1), 1),
+    ((0, 4096, 1, 1), 0),
+]
+
+
+@pytest.mark.parametrize("dom,mode", CASES_1D)
+def test_forasync1d_iteration_set_matches_reference(dom, mode):
+    import torch
+
+    base, ext = -8, 1200 if dom[1] < 1100 else 4200
+    counts = torch.zeros(ext, dtype=torch.int32, device="cuda")
+    args = H.VisitArgs(counts.data_ptr(), (C.c_int * 3)(base, 0, 0), (C.c_int * 3)(ext, 1, 1))
+    got_dom = H.forasync(H.BODY_VISIT_COUNT, args, [dom], mode)
+    torch.cuda.synchronize()
+    tiles, exp = L.forasync_nd_counts([dom], mode, H.num_workers(), [base], [ext])
+    assert got_dom[0][3] == tiles[0]
+    assert np.array_equal(counts.cpu().numpy(), exp)
+
+
+CASES_ND = [
+    ([(0, 30, 1, 7), (0, 20, 2, 3)], 0), ([(0, 30, 1, 7), (0, 20, 2, 3)], 1),
+    ([(2, 17, 3, 4), (1, 9, 1, 2), (0, 5, 2, 2)], 0), ([(2, 17, 3, 4), (1, 9, 1, 2), (0, 5, 2, 2)], 1),
+    ([(0, 64, 1, -1), (0, 64, 1, -1)], 0),
+]
+
+
+@pytest.mark.parametrize("doms,mode", CASES_ND)
+def test_forasync_nd_iteration_set_matches_reference(doms, mode):
+    import torch
+
+    ext = [40, 24, 8][: len(doms)]
+    full = ext + [1] * (3 - len(ext))
+    counts = torch.zeros(int(np.prod(full)), dtype=torch.int32, device="cuda")
+    args = H.VisitArgs(counts.data_ptr(), (C.c_int * 3)(0, 0, 0), (C.c_int * 3)(*full))
+    got = H.forasync(H.BODY_VISIT_COUNT, args, doms, mode)
+    torch.cuda.synchronize()
+    tiles, exp = L.forasync_nd_counts(doms, mode, H.num_workers(), [0] * len(doms), ext)
+    assert [d[3] for d in got] == tiles
+    assert np.array_equal(counts.cpu().numpy().reshape(ext), exp)
+
+
+# ----------------------------------------------------------------------- UTS
+@pytest.mark.parametrize("name", ["T1", "T2", "T3", "T4", "T5"])
+def test_uts_small_trees_bit_exact(golden, name):
+    g = golden("uts_goldens.json")
+    pub = g["published"][name]
+    r = H.uts(pub["args"], max_levels=pub["depth"] + 1 if pub["depth"] < 1000 else 0)
+    assert (r["nodes"], r["leaves"], r["max_depth"]) == (pub["nodes"], pub["leaves"], pub["depth"])
+    if name in g["levels"]:
+        assert r["levels"] == g["levels"][name]
+
+
+def test_uts_repeatable():
+    a = H.uts("-t 1 -a 3 -d 10 -b 4 -r 19")
+    b = H.uts("-t 1 -a 3 -d 10 -b 4 -r 19")
+    assert (a["nodes"], a["leaves"], a["max_depth"]) == (b["nodes"], b["leaves"], b["max_depth"])
+
+
+@pytest.mark.parametrize("name", ["T3L", "T1L"])
+def test_uts_large_trees_bit_exact(golden, name):
+    pub = golden("uts_goldens.json")["published"][name]
+    r = H.uts(pub["args"])
+    assert (r["nodes"], r["leaves"], r["max_depth"]) == (pub["nodes"], pub["leaves"], pub["depth"])
+
+
+@pytest.mark.parametrize("nshards,split", [(2, 3), (3, 5), (8, 6)])
+def test_uts_shards_sum_to_tree(golden, nshards, split):
+    pub = golden("uts_goldens.json")["published"]["T1"]
+    parts = [H.uts(pub["args"], s, nshards, split) for s in range(nshards)]
+    assert sum(p["nodes"] for p in parts) == pub["nodes"]
+    assert sum(p["leaves"] for p in parts) == pub["leaves"]
+    assert max(p["max_depth"] for p in parts) == pub["depth"]
+
+
+def test_uts_t3l_shards_sum_to_tree(golden):
+    pub = golden("uts_goldens.json")["published"]["T3L"]
+    parts = [H.uts(pub["args"], s, 4, 2000) for s in range(4)]
+    assert sum(p["nodes"] for p in parts) == pub["nodes"]
+    assert sum(p["leaves"] for p in parts) == pub["leaves"]
+    assert max(p["max_depth"] for p in parts) == pub["depth"]
+
+
+def test_uts_other_shapes_vs_oracle():
+    for args in ["-t 1 -a 1 -d 8 -b 3 -r 5", "-t 3 -d 6 -b 5 -r 3", "-t 0 -b 200 -q 0.19 -m 5 -r 11",
+                 "-t 1 -a 3 -d 7 -b 4 -r 19 -g 3"]:
+        (n, lv, d), _ = L.uts_serial(L.parse_uts_args(args))
+        r = H.uts(args)
+        assert (r["nodes"], r["leaves"], r["max_depth"]) == (n, lv, d), args
+
+
+# ----------------------------------------------------------------------- fib
+def test_fib_table(golden):
+    vals = golden("fib_goldens.json")["values"]
+    for n in [0, 1, 2, 3, 10, 20, 25]:
+        v, _ = H.fib(n)
+        assert v == vals[str(n)]
+
+
+def test_fib30_tasks_and_joins():
+    v, st = H.fib(30)
+    assert v == 832040
+    assert st["tasks"] == 2 * 1346269 - 1  # every fib call is one task
+    assert st["joins"] == 1346269 - 1      # one finish scope per internal call
+
+
+# ------------------------------------------------------------------------ SW
+def _sw_inputs(size):
+    a = open(os.path.join(GOLD, "sw", f"string1-{size}.txt"), "rb").read()
+    b = open(os.path.join(GOLD, "sw", f"string2-{size}.txt"), "rb").read()
+    return H.sw_map(a), H.sw_map(b)
+
+
+@pytest.mark.parametrize("size", ["tiny", "medium", "large", "huge"])
+def test_sw_published_scores(golden, size):
+    g = golden("sw_goldens.json")["published"][size]
+    s1, s2 = _sw_inputs(size)
+    score, st = H.sw(s1, s2, g["tile_w"], g["tile_h"])
+    assert score == g["score"]
+    assert st["tiles"] == (len(s1) // g["tile_w"]) * (len(s2) // g["tile_h"])
+
+
+def test_sw_oracle_configs(golden):
+    for cfg in golden("sw_goldens.json")["configs"]:
+        s1, s2 = _sw_inputs(cfg["input"])
+        s1, s2 = s1[: cfg["len1"]], s2[: cfg["len2"]]
+        score, _ = H.sw(s1, s2, cfg["tile_w"], cfg["tile_h"])
+        assert score == cfg["score"], cfg
+
+
+def test_sw_64k_golden(golden):
+    g = golden("sw_goldens.json")["sw64k"]
+    s1, s2 = _sw_inputs("huge")
+    score, st = H.sw(s1[:65536], s2[:65536], 256, 256)
+    assert score == g["score"] == 128772
+    assert st["tiles"] == 65536
+    assert st["releases"] == 3 * 255 * 255 + 2 * 255
+
+
+def test_sw_random_vs_oracle():
+    rng = np.random.default_rng(5)
+    for (n1, n2, tw, th) in [(300, 200, 17, 13), (1000, 777, 64, 300), (513, 1025, 256, 64)]:
+        s1 = bytes(rng.integers(1, 5, n1, dtype=np.int8).tobytes())
+        s2 = bytes(rng.integers(1, 5, n2, dtype=np.int8).tobytes())
+        score, _ = H.sw(s1, s2, tw, th)
+        assert score == L.sw_score(s1, s2, tw, th)
