@@ -41,59 +41,6 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def setup_dist(n_gpus):
-    import torch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != n_gpus:
-        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    if world > 1:
-        import torch.distributed as dist
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return rank, world, local
-
-
-def barrier(world):
-    import torch
-
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.barrier()
-    torch.cuda.synchronize()
-
-
-def allreduce_counts(world, nodes, leaves, depth):
-    import torch
-
-    if world == 1:
-        return nodes, leaves, depth
-    import torch.distributed as dist
-
-    t = torch.tensor([nodes, leaves], dtype=torch.int64, device="cuda")
-    d = torch.tensor([depth], dtype=torch.int64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    dist.all_reduce(d, op=dist.ReduceOp.MAX)
-    return int(t[0]), int(t[1]), int(d[0])
-
-
-def max_over_ranks(world, x):
-    import torch
-
-    if world == 1:
-        return x
-    import torch.distributed as dist
-
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t[0])
-
-
 def uts_step(H, rank, world, split):
     r = H.uts(T3L, rank, world, split) if world > 1 else H.uts(T3L)
     return r
@@ -167,14 +114,18 @@ def main():
 
     import torch  # noqa: F401  (one HIP runtime for torch + the module)
 
-    rank, world, local = setup_dist(args.gpus)
+    from hclib_amd import dist
+
+    rank, world, local = dist.init_from_env("nccl")
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     import hclib_amd as H
 
     H.init(local)
 
     for _ in range(args.warmup):
         r = uts_step(H, rank, world, args.split)
-    barrier(world)
+    dist.barrier(world)
     t0 = time.perf_counter()
     kernel_ms = []
     last = None
@@ -182,13 +133,14 @@ def main():
         r = uts_step(H, rank, world, args.split)
         kernel_ms.append(r["kernel_ms"])
         last = r
-    barrier(world)
-    elapsed = max_over_ranks(world, time.perf_counter() - t0)
-    tot = allreduce_counts(world, last["nodes"], last["leaves"], last["max_depth"])
+    dist.barrier(world)
+    elapsed = dist.max_over_ranks(time.perf_counter() - t0, world)
+    tot = dist.combine_counts(last["nodes"], last["leaves"], last["max_depth"], world)
     if tot != T3L_GOLD:
         raise SystemExit(f"T3L mismatch: {tot} != {T3L_GOLD}")
     value = T3L_GOLD[0] * args.steps / elapsed
     if rank != 0:
+        dist.shutdown(world)
         return
 
     out = {
@@ -255,6 +207,7 @@ def main():
         threads = max(1, min(threads, 16, os.cpu_count() or 1))
         out["cpu_baseline"] = cpu_baseline(threads)
     print(json.dumps(out), flush=True)
+    dist.shutdown(world)
 
 
 if __name__ == "__main__":

@@ -58,13 +58,14 @@ class UtsResult(C.Structure):
     _fields_ = [
         ("nodes", C.c_uint64), ("leaves", C.c_uint64), ("max_depth", C.c_uint64),
         ("chunks_pushed", C.c_uint64), ("chunks_stolen", C.c_uint64), ("batches", C.c_uint64),
-        ("kernel_ms", C.c_double),
+        ("kernel_ms", C.c_double), ("busy_frac", C.c_double), ("us_per_batch", C.c_double),
     ]
 
 
 class FibResult(C.Structure):
     _fields_ = [("tasks", C.c_uint64), ("joins", C.c_uint64), ("chunks_pushed", C.c_uint64),
-                ("chunks_stolen", C.c_uint64), ("kernel_ms", C.c_double)]
+                ("chunks_stolen", C.c_uint64), ("kernel_ms", C.c_double),
+                ("busy_frac", C.c_double)]
 
 
 class SwResult(C.Structure):

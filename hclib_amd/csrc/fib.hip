@@ -152,14 +152,15 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     HX_HIP(hipMemsetAsync(ctx.join_next, 0, 256, m.stream));
     PoolView pool;
     HX_TRY(make_pool((uint32_t)env_int("HCLIB_HIP_DEQUES", 64),
-                     (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
-                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 32), FibKind::kWords, &pool));
+                     (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 16384),
+                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 8), FibKind::kWords, &pool));
+    const int grid = m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);
     SchedConfig cfg;
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_HI", 256);
-    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", 8);
+    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", 2);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
+    cfg.nwaves = (uint32_t)grid;
     HX_TRY(reset_sched(pool, 1));
-    const int grid = m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 8);
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     hipLaunchKernelGGL(k_fib, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
     HX_HIP(hipGetLastError());
@@ -176,9 +177,12 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     if (result) {
         result->tasks = gl.counters[0];
         result->joins = gl.counters[1];
-        result->chunks_pushed = gl.counters[14];
-        result->chunks_stolen = gl.counters[15];
+        result->chunks_pushed = gl.counters[kCtrPushed];
+        result->chunks_stolen = gl.counters[kCtrStolen];
         result->kernel_ms = ms;
+        const double busy = (double)gl.counters[kCtrBusyCycles],
+                     idle = (double)gl.counters[kCtrIdleCycles];
+        result->busy_frac = (busy + idle) > 0 ? busy / (busy + idle) : 0.0;
     }
     return HCLIB_HIP_OK;
 }

@@ -26,43 +26,70 @@ __device__ __forceinline__ float triad1(float b, float c, float s) {
 }
 
 constexpr int kTriadThreads = 256;
-constexpr int kTriadUnroll = 4;  // float4 loads in flight per lane per operand
+typedef float v4f __attribute__((ext_vector_type(4)));
 
+template <bool NT>
+__device__ __forceinline__ v4f ld4(const v4f *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st4(v4f v, v4f *p) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// Grid-stride tiles of 16 B per lane; UNROLL independent (b, c) pairs per
+// lane in flight; NTL / NTS select non-temporal loads / stores.
+template <bool NTL, bool NTS, int UNROLL>
 __global__ __launch_bounds__(kTriadThreads) void k_triad_f32(float *__restrict__ a,
                                                              const float *__restrict__ b,
                                                              const float *__restrict__ c, float s,
                                                              int64_t n4) {
-    typedef float v4f __attribute__((ext_vector_type(4)));
     const int64_t stride = (int64_t)gridDim.x * kTriadThreads;
     int64_t i = (int64_t)blockIdx.x * kTriadThreads + threadIdx.x;
     const v4f *b4 = reinterpret_cast<const v4f *>(b);
     const v4f *c4 = reinterpret_cast<const v4f *>(c);
     v4f *a4 = reinterpret_cast<v4f *>(a);
-    // main loop: kTriadUnroll independent 16-B pairs per lane in flight
-    for (; i + (kTriadUnroll - 1) * stride < n4; i += kTriadUnroll * stride) {
-        v4f vb[kTriadUnroll], vc[kTriadUnroll];
+    for (; i + (UNROLL - 1) * stride < n4; i += UNROLL * stride) {
+        v4f vb[UNROLL], vc[UNROLL];
 #pragma unroll
-        for (int u = 0; u < kTriadUnroll; ++u) {
-            vb[u] = __builtin_nontemporal_load(&b4[i + u * stride]);
-            vc[u] = __builtin_nontemporal_load(&c4[i + u * stride]);
+        for (int u = 0; u < UNROLL; ++u) {
+            vb[u] = ld4<NTL>(&b4[i + u * stride]);
+            vc[u] = ld4<NTL>(&c4[i + u * stride]);
         }
 #pragma unroll
-        for (int u = 0; u < kTriadUnroll; ++u) {
+        for (int u = 0; u < UNROLL; ++u) {
             v4f r;
             r.x = triad1(vb[u].x, vc[u].x, s);
             r.y = triad1(vb[u].y, vc[u].y, s);
             r.z = triad1(vb[u].z, vc[u].z, s);
             r.w = triad1(vb[u].w, vc[u].w, s);
-            __builtin_nontemporal_store(r, &a4[i + u * stride]);
+            st4<NTS>(r, &a4[i + u * stride]);
         }
     }
     for (; i < n4; i += stride) {
-        v4f vb = b4[i], vc = c4[i], r;
+        v4f vb = ld4<NTL>(&b4[i]), vc = ld4<NTL>(&c4[i]), r;
         r.x = triad1(vb.x, vc.x, s);
         r.y = triad1(vb.y, vc.y, s);
         r.z = triad1(vb.z, vc.z, s);
         r.w = triad1(vb.w, vc.w, s);
-        __builtin_nontemporal_store(r, &a4[i]);
+        st4<NTS>(r, &a4[i]);
+    }
+}
+
+typedef void (*triad_kernel_t)(float *, const float *, const float *, float, int64_t);
+// variant bits: 1 = nt loads, 2 = nt stores, 4 = unroll 8 (else 4)
+static triad_kernel_t triad_variant(int v) {
+    switch (v & 7) {
+    case 0: return k_triad_f32<false, false, 4>;
+    case 1: return k_triad_f32<true, false, 4>;
+    case 2: return k_triad_f32<false, true, 4>;
+    case 3: return k_triad_f32<true, true, 4>;
+    case 4: return k_triad_f32<false, false, 8>;
+    case 5: return k_triad_f32<true, false, 8>;
+    case 6: return k_triad_f32<false, true, 8>;
+    default: return k_triad_f32<true, true, 8>;
     }
 }
 
@@ -208,12 +235,12 @@ extern "C" int hclib_hip_forasync_triad_f32(float *a, const float *b, const floa
     }
     const int64_t n4 = n / 4;
     if (n4 > 0) {
-        const int bpc = env_int("HCLIB_HIP_TRIAD_BLOCKS_PER_CU", 8);
+        const int bpc = env_int("HCLIB_HIP_TRIAD_BLOCKS_PER_CU", 2);
         int64_t grid = (int64_t)mod().num_cus * bpc;
         const int64_t need = (n4 + kTriadThreads - 1) / kTriadThreads;
         if (grid > need) grid = need;
-        hipLaunchKernelGGL(k_triad_f32, dim3((unsigned)grid), dim3(kTriadThreads), 0, st, a, b, c,
-                           s, n4);
+        hipLaunchKernelGGL(triad_variant(env_int("HCLIB_HIP_TRIAD_VARIANT", 7)),
+                           dim3((unsigned)grid), dim3(kTriadThreads), 0, st, a, b, c, s, n4);
         HX_HIP(hipGetLastError());
     }
     if (n4 * 4 < n) {

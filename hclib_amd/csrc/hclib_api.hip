@@ -1,0 +1,528 @@
+// hclib_api.hip — the HClib C API (include/hclib.h) on top of modules/hip.
+//
+// The host side of the MI355X runtime is a single control thread: the
+// scheduler that matters runs on the GPU. This file keeps the reference's
+// task model exactly where it is observable — finish counters
+// (src/hclib-runtime.c:431-446, 1219-1313), promises with waiter lists and
+// chained registration over a task's futures (src/hclib-promise.c:132-245),
+// forasync tile-size rules (src/hclib.c:452-473) — and routes the work:
+//   * device task kinds (fib, UTS) -> one persistent megakernel launch each
+//     (uts.hip / fib.hip), their results written back into the task's own
+//     argument struct when the task completes;
+//   * device loop bodies -> one grid-stride sweep launch (forasync.hip);
+//   * any other function -> a host task run by the control thread, help-first
+//     inside end_finish / future_wait (the reference's work-shift,
+//     src/hclib-runtime.c:1067-1119; no fibers needed with one thread).
+// Errors abort with a message, like HASSERT / log_die in the reference.
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/hclib.h"
+#include "hx_module.h"
+
+struct hclib_locale_t {
+    int id;      // 0 = host (sysmem), 1.. = GPU index + 1
+    int gpu;     // HIP device index or -1
+};
+
+// finish_t, src/inc/hclib-finish.h:6-10
+struct Finish {
+    Finish *parent;
+    int counter;
+    hclib_promise_t *finish_dep;
+};
+
+struct hclib_task_t {
+    generic_frame_ptr fp;
+    void *args;
+    Finish *finish;
+    hclib_future_t *waiting_on[MAX_NUM_WAITS];
+    std::vector<hclib_future_t *> *extra;
+    int waiting_on_index;
+    int device_kind;  // 0 = host task
+    hclib_task_t *next_waiter;
+};
+
+namespace {
+
+#define SENTINEL ((hclib_task_t *)0x1)
+#define SATISFIED ((hclib_task_t *)0x2)
+
+struct Runtime {
+    bool launched = false;
+    bool hip = false;
+    Finish *current = nullptr;
+    std::vector<hclib_task_t *> ready;  // LIFO, like the owner end of a deque
+    std::map<generic_frame_ptr, int> kinds;
+    std::map<void *, int> bodies;
+    hclib_locale_t host{0, -1};
+    hclib_locale_t gpu{1, 0};
+    // stats (HCLIB_STATS analogue, src/hclib-runtime.c:83-104)
+    unsigned long long host_tasks = 0, device_tasks = 0, end_finishes = 0, forasyncs = 0;
+    unsigned long long device_items = 0;
+    double device_ms = 0;
+};
+
+Runtime &rt() {
+    static Runtime r;
+    return r;
+}
+
+[[noreturn]] void die(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    fprintf(stderr, "hclib: ");
+    vfprintf(stderr, fmt, ap);
+    fprintf(stderr, "\n");
+    va_end(ap);
+    abort();
+}
+
+struct ModuleHooks {
+    std::string name;
+    hclib_module_pre_init_func_type pre;
+    hclib_module_post_init_func_type post;
+    hclib_module_finalize_func_type fin;
+};
+std::vector<ModuleHooks> &modules() {
+    static std::vector<ModuleHooks> m;
+    return m;
+}
+
+void check_in(Finish *f) {
+    if (f) f->counter++;
+}
+
+void check_out(Finish *f) {
+    if (f && --f->counter == 0 && f->finish_dep) hclib_promise_put(f->finish_dep, f);
+}
+
+// _register_if_promise_not_ready, src/hclib-promise.c:132-166
+bool register_if_not_ready(hclib_task_t *t, hclib_future_t *fut) {
+    hclib_promise_t *p = fut->owner;
+    if (p->wait_list_head == SATISFIED) return false;
+    t->next_waiter = p->wait_list_head;
+    p->wait_list_head = t;
+    return true;
+}
+
+// register_on_all_promise_dependencies, src/hclib-promise.c:171-195
+bool register_all(hclib_task_t *t) {
+    while (t->waiting_on_index < MAX_NUM_WAITS - 1) {
+        t->waiting_on_index++;
+        hclib_future_t *f = t->waiting_on[t->waiting_on_index];
+        if (f && register_if_not_ready(t, f)) return false;
+    }
+    if (t->extra) {
+        while (t->waiting_on_index - MAX_NUM_WAITS + 1 < (int)t->extra->size()) {
+            t->waiting_on_index++;
+            hclib_future_t *f = (*t->extra)[t->waiting_on_index - MAX_NUM_WAITS];
+            if (register_if_not_ready(t, f)) return false;
+        }
+    }
+    return true;
+}
+
+void make_ready(hclib_task_t *t) { rt().ready.push_back(t); }
+
+int check_hip(int rc, const char *what) {
+    if (rc != HCLIB_HIP_OK) die("%s failed: %s", what, hclib_hip_last_error());
+    return rc;
+}
+
+void ensure_gpu(const char *who) {
+    if (!rt().hip) {
+        // device kinds need the "hip" module; load it on first use, as the
+        // reference dlopens modules named in deps (src/hclib-runtime.c:294-317)
+        if (hclib_hip_init(hx::env_int("HCLIB_HIP_DEVICE", hx::env_int("LOCAL_RANK", 0))) !=
+            HCLIB_HIP_OK)
+            die("%s: the hip module could not bind a gfx950 device: %s", who,
+                hclib_hip_last_error());
+        rt().hip = true;
+    }
+}
+
+// run one device task kind to completion and write its outputs back
+void run_device_task(hclib_task_t *t) {
+    Runtime &R = rt();
+    ensure_gpu("device task");
+    R.device_tasks++;
+    switch (t->device_kind) {
+    case HCLIB_HIP_KIND_FIB: {
+        // FibArgs of test/fib/fib.c:50-53: { int n; long res; }
+        struct FibArgs {
+            int n;
+            long res;
+        } *a = (FibArgs *)t->args;
+        int64_t v = 0;
+        hclib_hip_fib_result_t r;
+        check_hip(hclib_hip_fib(a->n, &v, &r), "hclib_hip_fib");
+        a->res = (long)v;
+        R.device_items += r.tasks;
+        R.device_ms += r.kernel_ms;
+        break;
+    }
+    case HCLIB_HIP_KIND_UTS: {
+        hclib_hip_uts_task_t *a = (hclib_hip_uts_task_t *)t->args;
+        hclib_hip_uts_params_t p;
+        p.type = a->type;
+        p.shape_fn = a->shape_fn;
+        p.gen_mx = a->gen_mx;
+        p.root_id = a->root_id;
+        p.non_leaf_bf = a->non_leaf_bf;
+        p.compute_gran = a->compute_gran;
+        p.b_0 = a->b_0;
+        p.non_leaf_prob = a->non_leaf_prob;
+        p.shift_depth = a->shift_depth;
+        hclib_hip_uts_result_t r;
+        check_hip(hclib_hip_uts_search(&p, 0, 1, 0, &r, nullptr, 0), "hclib_hip_uts_search");
+        a->nodes = r.nodes;
+        a->leaves = r.leaves;
+        a->max_depth = r.max_depth;
+        R.device_items += r.nodes;
+        R.device_ms += r.kernel_ms;
+        break;
+    }
+    default:
+        die("unknown device task kind %d", t->device_kind);
+    }
+}
+
+// execute_task, src/hclib-runtime.c:448-478
+void execute(hclib_task_t *t) {
+    Runtime &R = rt();
+    Finish *saved = R.current;
+    R.current = t->finish;
+    if (t->device_kind) {
+        run_device_task(t);
+    } else {
+        R.host_tasks++;
+        t->fp(t->args);
+    }
+    R.current = saved;
+    check_out(t->finish);
+    delete t->extra;
+    free(t);
+}
+
+// find_and_run_task with one worker: pop the newest ready task
+bool run_one() {
+    Runtime &R = rt();
+    if (R.ready.empty()) return false;
+    hclib_task_t *t = R.ready.back();
+    R.ready.pop_back();
+    execute(t);
+    return true;
+}
+
+void spawn(generic_frame_ptr fp, void *arg, hclib_future_t **futures, int nfutures) {
+    Runtime &R = rt();
+    if (!R.launched) die("hclib_async called outside hclib_launch");
+    hclib_task_t *t = (hclib_task_t *)calloc(1, sizeof(hclib_task_t));
+    if (!t) die("out of memory");
+    t->fp = fp;
+    t->args = arg;
+    auto k = R.kinds.find(fp);
+    t->device_kind = (k == R.kinds.end()) ? 0 : k->second;
+    t->finish = R.current;
+    check_in(t->finish);
+    t->waiting_on_index = -1;
+    for (int i = 0; i < nfutures && i < MAX_NUM_WAITS; ++i) t->waiting_on[i] = futures[i];
+    if (nfutures > MAX_NUM_WAITS) {
+        t->extra = new std::vector<hclib_future_t *>(futures + MAX_NUM_WAITS, futures + nfutures);
+    }
+    if (nfutures == 0 || register_all(t)) make_ready(t);
+}
+
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------ lifecycle
+int hclib_add_module_init_function(const char *lbl, hclib_module_pre_init_func_type pre,
+                                   hclib_module_post_init_func_type post,
+                                   hclib_module_finalize_func_type finalize) {
+    modules().push_back(ModuleHooks{lbl ? lbl : "", pre, post, finalize});
+    return 0;
+}
+
+void hclib_init(const char **deps, int ndeps, const int instrument) {
+    (void)instrument;
+    Runtime &R = rt();
+    if (R.launched) die("hclib_init called twice");
+    for (auto &m : modules())
+        if (m.pre) m.pre();
+    for (int i = 0; i < ndeps; ++i) {
+        const char *d = deps[i];
+        if (!strcmp(d, "hip") || !strcmp(d, "gpu")) {
+            ensure_gpu("hclib_init");
+        } else if (strcmp(d, "system") != 0) {
+            fprintf(stderr, "WARNING: hclib module \"%s\" is not available in this build\n", d);
+        }
+    }
+    for (auto &m : modules())
+        if (m.post) m.post();
+    R.launched = true;
+    hclib_start_finish();  // root finish (src/hclib-runtime.c:400)
+}
+
+void hclib_finalize(const int instrument) {
+    (void)instrument;
+    Runtime &R = rt();
+    hclib_end_finish();
+    for (auto &m : modules())
+        if (m.fin) m.fin();
+    R.launched = false;
+    const char *stats = getenv("HCLIB_STATS");
+    if (stats && *stats && strcmp(stats, "0")) hclib_print_runtime_stats(stdout);
+}
+
+void hclib_launch(async_fct_t fct_ptr, void *arg, const char **deps, int ndeps) {
+    const char *prof = getenv("HCLIB_PROFILE_LAUNCH_BODY");
+    hclib_init(deps, ndeps, 0);
+    const unsigned long long t0 = hclib_current_time_ns();
+    hclib_async(fct_ptr, arg, nullptr, 0, nullptr);  // src/hclib-runtime.c:1472
+    hclib_finalize(0);  // ends the root finish: the root task runs here
+    const unsigned long long t1 = hclib_current_time_ns();
+    if (prof && *prof) printf("\nHCLIB TIME %llu ns\n", t1 - t0);
+}
+
+unsigned long long hclib_current_time_ns(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (unsigned long long)ts.tv_sec * 1000000000ull + ts.tv_nsec;
+}
+
+unsigned long long hclib_current_time_ms(void) { return hclib_current_time_ns() / 1000000ull; }
+
+// ---------------------------------------------------------------- tasks
+void hclib_async(generic_frame_ptr fp, void *arg, hclib_future_t **futures, const int nfutures,
+                 hclib_locale_t *locale) {
+    (void)locale;  // device kinds run on the GPU locale, everything else on the host
+    spawn(fp, arg, futures, nfutures);
+}
+
+void hclib_async_nb(generic_frame_ptr fp, void *arg, hclib_locale_t *locale) {
+    hclib_async(fp, arg, nullptr, 0, locale);
+}
+
+namespace {
+struct FutureWrapper {
+    hclib_promise_t event;
+    future_fct_t fp;
+    void *in;
+};
+void future_caller(void *raw) {  // src/hclib.c:65-69
+    FutureWrapper *w = (FutureWrapper *)raw;
+    void *r = w->fp(w->in);
+    hclib_promise_put(&w->event, r);
+}
+}  // namespace
+
+hclib_future_t *hclib_async_future(future_fct_t fp, void *arg, hclib_future_t **futures,
+                                   const int nfutures, hclib_locale_t *locale) {
+    FutureWrapper *w = (FutureWrapper *)malloc(sizeof(FutureWrapper));
+    hclib_promise_init(&w->event);
+    w->fp = fp;
+    w->in = arg;
+    hclib_async(future_caller, w, futures, nfutures, locale);
+    return &w->event.future;
+}
+
+// hclib_start_finish, src/hclib-runtime.c:1219-1247
+void hclib_start_finish(void) {
+    Runtime &R = rt();
+    Finish *f = (Finish *)calloc(1, sizeof(Finish));
+    f->counter = 1;
+    f->parent = R.current;
+    check_in(f->parent);
+    R.current = f;
+}
+
+// hclib_end_finish + help_finish, src/hclib-runtime.c:1249-1277, 1067-1119
+void hclib_end_finish(void) {
+    Runtime &R = rt();
+    Finish *f = R.current;
+    if (!f) die("hclib_end_finish without a matching start");
+    R.end_finishes++;
+    while (f->counter > 1) {
+        if (!run_one())
+            die("end_finish: %d task(s) wait on promises that nothing can put (deadlock)",
+                f->counter - 1);
+    }
+    R.current = f->parent;
+    check_out(f->parent);
+    free(f);
+}
+
+// src/hclib-runtime.c:1280-1313
+void hclib_end_finish_nonblocking_helper(hclib_promise_t *event) {
+    Runtime &R = rt();
+    Finish *f = R.current;
+    f->finish_dep = event;
+    R.current = f->parent;
+    check_out(f);  // the owner's check-out; puts `event` when the scope drains
+    check_out(f->parent);
+}
+
+hclib_future_t *hclib_end_finish_nonblocking(void) {
+    hclib_promise_t *e = hclib_promise_create();
+    hclib_end_finish_nonblocking_helper(e);
+    return &e->future;
+}
+
+// ------------------------------------------------------------- forasync
+void hclib_forasync(void *fct, void *argv, int dim, hclib_loop_domain_t *domain,
+                    forasync_mode_t mode) {
+    Runtime &R = rt();
+    auto b = R.bodies.find(fct);
+    if (b == R.bodies.end())
+        die("hclib_forasync: %p is not a registered device loop body "
+            "(hclib_hip_register_forasync_body); forasync runs on the GPU only", fct);
+    ensure_gpu("hclib_forasync");
+    R.forasyncs++;
+    static_assert(sizeof(hclib_loop_domain_t) == sizeof(hclib_hip_loop_domain_t), "layout");
+    hclib_hip_loop_domain_t *d = (hclib_hip_loop_domain_t *)domain;
+    int rc;
+    if (b->second == HCLIB_HIP_BODY_IOTA_CHECK) {
+        // test/c/forasync1DCh.c passes a plain host int array: map it for the sweep
+        hclib_hip_loop_domain_t dd = d[0];
+        if (dd.tile == -1) dd.tile = ((dd.high - dd.low) + hclib_get_num_workers() - 1) /
+                                     hclib_get_num_workers();
+        const size_t extent = (size_t)(dd.high + (dd.tile > 0 ? dd.tile : 1));
+        int *dev_ran = nullptr, *dev_err = nullptr;
+        if (hipMalloc((void **)&dev_ran, extent * sizeof(int)) != hipSuccess ||
+            hipMalloc((void **)&dev_err, sizeof(int)) != hipSuccess)
+            die("hclib_forasync: device allocation failed");
+        (void)hipMemcpy(dev_ran, argv, (size_t)dd.high * sizeof(int), hipMemcpyHostToDevice);
+        (void)hipMemset(dev_err, 0, sizeof(int));
+        hclib_hip_iota_args_t ia = {dev_ran, dev_err};
+        rc = hclib_hip_forasync(b->second, &ia, dim, d, mode, nullptr);
+        (void)hipDeviceSynchronize();
+        int nerr = 0;
+        (void)hipMemcpy(argv, dev_ran, (size_t)dd.high * sizeof(int), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(&nerr, dev_err, sizeof(int), hipMemcpyDeviceToHost);
+        (void)hipFree(dev_ran);
+        (void)hipFree(dev_err);
+        if (nerr) die("forasync body check failed at %d indices", nerr);
+    } else {
+        rc = hclib_hip_forasync(b->second, argv, dim, d, mode, nullptr);
+        (void)hipDeviceSynchronize();  // the sweep belongs to the enclosing finish
+    }
+    check_hip(rc, "hclib_hip_forasync");
+}
+
+hclib_future_t *hclib_forasync_future(void *fct, void *argv, int dim,
+                                      hclib_loop_domain_t *domain, forasync_mode_t mode) {
+    hclib_start_finish();  // src/hclib.c:466-473
+    hclib_forasync(fct, argv, dim, domain, mode);
+    return hclib_end_finish_nonblocking();
+}
+
+// ------------------------------------------------------------- promises
+void hclib_promise_init(hclib_promise_t *p) {
+    p->satisfied = 0;
+    p->datum = nullptr;
+    p->wait_list_head = SENTINEL;
+    p->future.owner = p;
+}
+
+hclib_promise_t *hclib_promise_create(void) {
+    hclib_promise_t *p = (hclib_promise_t *)malloc(sizeof(hclib_promise_t));
+    if (!p) die("out of memory");
+    hclib_promise_init(p);
+    return p;
+}
+
+hclib_future_t *hclib_get_future_for_promise(hclib_promise_t *p) { return &p->future; }
+
+hclib_promise_t **hclib_promise_create_n(size_t n, int null_terminated) {
+    hclib_promise_t **ps = (hclib_promise_t **)malloc(sizeof(hclib_promise_t *) * n);
+    const size_t lg = null_terminated ? n - 1 : n;
+    for (size_t i = 0; i < lg; ++i) ps[i] = hclib_promise_create();
+    if (null_terminated) ps[lg] = nullptr;
+    return ps;
+}
+
+void hclib_promise_free_n(hclib_promise_t **ps, size_t n, int null_terminated) {
+    const size_t lg = null_terminated ? n - 1 : n;
+    for (size_t i = 0; i < lg; ++i) hclib_promise_free(ps[i]);
+    free(ps);
+}
+
+void hclib_promise_free(hclib_promise_t *p) { free(p); }
+
+void *hclib_future_get(hclib_future_t *f) {
+    if (!f->owner->satisfied) die("hclib_future_get on an unsatisfied future");
+    return f->owner->datum;
+}
+
+// hclib_promise_put, src/hclib-promise.c:203-245
+void hclib_promise_put(hclib_promise_t *p, void *datum) {
+    if (p->satisfied) die("violated single assignment property for promises");
+    p->datum = datum;
+    p->satisfied = 1;
+    hclib_task_t *list = p->wait_list_head;
+    p->wait_list_head = SATISFIED;
+    while (list != SENTINEL) {
+        hclib_task_t *next = list->next_waiter;
+        if (register_all(list)) make_ready(list);
+        list = next;
+    }
+}
+
+// hclib_future_wait, src/hclib-runtime.c:983-1025 (help while waiting)
+void *hclib_future_wait(hclib_future_t *f) {
+    while (!f->owner->satisfied) {
+        if (!run_one()) die("future_wait: the future can never be satisfied (deadlock)");
+    }
+    return f->owner->datum;
+}
+
+int hclib_future_is_satisfied(hclib_future_t *f) { return f->owner->satisfied; }
+
+// -------------------------------------------------------------- queries
+int hclib_get_num_workers(void) {
+    const int n = hclib_hip_num_workers();
+    return n > 0 ? n : 1;
+}
+
+int hclib_get_current_worker(void) { return 0; }
+
+hclib_locale_t *hclib_get_closest_locale(void) { return &rt().host; }
+
+hclib_locale_t *hclib_hip_gpu_locale(int index) {
+    rt().gpu.gpu = index;
+    return &rt().gpu;
+}
+
+void hclib_hip_register_async_kind(generic_frame_ptr fp, int kind) {
+    if (kind != HCLIB_HIP_KIND_FIB && kind != HCLIB_HIP_KIND_UTS)
+        die("hclib_hip_register_async_kind: unknown kind %d", kind);
+    rt().kinds[fp] = kind;
+}
+
+void hclib_hip_register_forasync_body(void *fct, int body) {
+    if (body < HCLIB_HIP_BODY_TRIAD_F32 || body > HCLIB_HIP_BODY_VISIT_COUNT)
+        die("hclib_hip_register_forasync_body: unknown body %d", body);
+    rt().bodies[fct] = body;
+}
+
+// hclib_print_runtime_stats, src/hclib-runtime.c:1370-1410
+void hclib_print_runtime_stats(FILE *fp) {
+    Runtime &R = rt();
+    fprintf(fp,
+            "HCLIB STATS: host_tasks=%llu device_tasks=%llu device_items=%llu "
+            "device_ms=%.3f end_finishes=%llu forasyncs=%llu device_workers=%d\n",
+            R.host_tasks, R.device_tasks, R.device_items, R.device_ms, R.end_finishes,
+            R.forasyncs, hclib_hip_num_workers());
+}
+
+}  // extern "C"

@@ -5,22 +5,26 @@
 // wavefront-granular scheduler:
 //
 //   worker        = one 64-lane wave (one workgroup of 64 threads), resident
-//                   for the whole launch; ~8 per CU.
+//                   for the whole launch; a few per SIMD.
 //   local deque   = a ring of task entries in the wave's LDS (the "LDS-cached
 //                   hot end"); the owner pushes/pops at the top (LIFO,
 //                   work-first like ss_get_work, test/uts/UTS.cpp:383-402).
-//   spill/steal   = the oldest entries of a ring move, as one chunk, into an
-//                   HBM chunk deque (bounded MPMC ring, one per XCD slice);
-//                   idle waves take chunks from their own deque first, then
-//                   from deques of the same XCD, then anywhere — the
-//                   reference's intra-socket-first victim order
+//   spill/steal   = the oldest entries of a ring (the shallowest, largest
+//                   subtrees) move as one chunk into an HBM chunk deque
+//                   (bounded MPMC ring, two per XCD); idle waves take chunks
+//                   from their own XCD's deques first, then the last deque
+//                   pushed to, then anywhere — the reference's
+//                   intra-socket-first victim order
 //                   (src/hclib-locality-graph.c:864-884) mapped to XCDs.
 //   a "task"      = one lane-item: an entry carries a count of items
-//                   (children to spawn, or 1), the wave expands up to 64
-//                   items per batch (one per lane) by prefix sum.
+//                   (children to spawn, or 1); the wave expands up to 64 items
+//                   per batch (one per lane) by prefix sum (DPP wave scans).
 //   termination   = `outstanding` = chunks in deques + waves holding work;
 //                   the launch ends when it reads 0 (the finish counter of
 //                   src/hclib-runtime.c:431-446 for the whole launch).
+//   hunger        = waves - outstanding = waves with neither work nor a
+//                   queued chunk to take; a wave gives away its oldest
+//                   entries only while that is > 0 (no chunk floods).
 //
 // All cross-wave words use agent-scope atomics; chunk payloads are written
 // with sc1 stores and published behind s_waitcnt + release, consumed after an
@@ -45,12 +49,23 @@ struct alignas(256) QueueHdr {
 struct alignas(256) SchedGlobals {
     uint32_t outstanding;  // chunks queued + waves holding work
     uint32_t pad0[63];
-    uint32_t idle;  // waves currently without work (spill hint)
+    uint32_t hint;  // deque most recently pushed to
     uint32_t pad1[63];
     uint32_t err;  // DevError
     uint32_t pad2[63];
-    unsigned long long counters[16];  // kind-specific reductions (atomic adds)
+    unsigned long long counters[16];  // [0..7] kind-specific, [8..15] scheduler
     unsigned long long maxes[4];      // kind-specific reductions (atomic max)
+};
+
+// scheduler counters (SchedGlobals::counters)
+enum : int {
+    kCtrBusyCycles = 9,   // s_memtime cycles inside batches (all waves)
+    kCtrIdleCycles = 10,  // s_memtime cycles idle / stealing
+    kCtrSpillCycles = 11, // cycles inside enqueue
+    kCtrWaves = 12,
+    kCtrBatches = 13,
+    kCtrPushed = 14,
+    kCtrStolen = 15,
 };
 
 struct PoolView {
@@ -64,9 +79,10 @@ struct PoolView {
 };
 
 struct SchedConfig {
-    uint32_t spill_hi;   // always spill above this many entries
-    uint32_t spill_lo;   // spill above this when some wave is idle
+    uint32_t spill_hi;   // always spill above this many entries (ring capacity valve)
+    uint32_t spill_lo;   // give away entries to hungry waves when holding >= this many
     uint32_t spin_limit; // ms a wave may stay idle before declaring a timeout
+    uint32_t nwaves;     // waves in the launch (hunger = nwaves - outstanding)
 };
 
 // Kind concept:
@@ -85,6 +101,55 @@ struct WaveStack {
     uint32_t e[CAP][W];
     int own[kWaveSize];
 };
+
+// ------------------------------------------------------- DPP wave scans
+// Inclusive scans over the 64 lanes with DPP row shifts and row broadcasts
+// (GFX9 row_bcast:15/31), ~12 VALU ops, no LDS round trips.
+__device__ __forceinline__ int wave_scan_add(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ int wave_scan_max(int x) {  // identity -1 (x >= -1)
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+__device__ __forceinline__ int lane63(int x) { return __builtin_amdgcn_readlane(x, 63); }
+
+// Chunk hand-off. Every payload word is stored with an agent-scope (sc1,
+// write-through) store and loaded with an agent-scope (sc1) load, so the
+// form of MI355X_MICROARCH.md "Valid forms" applies: the producer drains
+// its stores (s_waitcnt vmcnt(0)) before the sequence word, the consumer
+// needs no L1 invalidate. HX_STRICT_HANDOFF=1 restores the release/acquire
+// fences (diagnostic build).
+#ifndef HX_STRICT_HANDOFF
+#define HX_STRICT_HANDOFF 0
+#endif
+__device__ __forceinline__ void handoff_publish() {
+#if HX_STRICT_HANDOFF
+    release_agent();
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+}
+__device__ __forceinline__ void handoff_consume() {
+#if HX_STRICT_HANDOFF
+    acquire_agent();
+#else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+#endif
+}
+__device__ __forceinline__ uint32_t lane0(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // Try to publish `n` entries (ring positions bot..bot+n-1) as one chunk into
 // deque q. Called by the whole wave; returns true if published.
@@ -123,8 +188,11 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
         st_agent(&dst[i], st.e[(bot + ent) & (CAP - 1)][w]);
     }
     if (lane == 0) st_agent(&pool.cnt[slot], n);
-    release_agent();
-    if (lane == 0) st_agent(&pool.seq[slot], pos + 1);
+    handoff_publish();
+    if (lane == 0) {
+        st_agent(&pool.seq[slot], pos + 1);
+        st_agent(&g->hint, q);
+    }
     return true;
 }
 
@@ -155,7 +223,7 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
     ok = __shfl(ok, 0, 64);
     if (!ok) return 0;
     pos = __shfl(pos, 0, 64);
-    acquire_agent();
+    handoff_consume();
     const uint32_t slot = q * pool.cap + (pos & (pool.cap - 1));
     const uint32_t n = ld_agent(&pool.cnt[slot]);
     const uint32_t *src = pool.data + (size_t)slot * pool.chunk * W;
@@ -185,10 +253,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     static_assert((CAP & (CAP - 1)) == 0, "CAP must be a power of two");
     const int lane = lane_id();
     const uint32_t gid = blockIdx.x;
-    const uint32_t nxcd = 8;
-    const uint32_t qpx = pool.nq / nxcd;
+    const uint32_t qpx = pool.nq / 8;
     const uint32_t xcc = xcc_id() & 7u;
-    const uint32_t home = xcc * qpx + (gid / nxcd) % qpx;
+    const uint32_t home = xcc * qpx + (gid / 8) % qpx;
     uint32_t rng = 0x9e3779b9u ^ (gid * 0x85ebca6bu + 1u);
 
     typename Kind::Acc acc;
@@ -197,6 +264,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     uint32_t spins = 0;
     unsigned long long idle_since = 0;
     unsigned long long nbatch = 0, npush = 0, nsteal = 0;
+    unsigned long long cyc_busy = 0, cyc_idle = 0, cyc_spill = 0;
 
     if (seed_roots) {
         uint32_t out[MO > 4 ? MO : 4][W];
@@ -213,25 +281,27 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         }
         __syncthreads();
     }
-    if (!active && lane == 0) add_agent(&g->idle, 1u);
 
+    unsigned long long t_mark = __builtin_amdgcn_s_memtime();
+    uint32_t outst_pf = 0;  // lane 0: `outstanding` as loaded one batch ago
     while (true) {
         const uint32_t size = top - bot;
         if (size == 0) {
             if (active) {
                 active = false;
-                if (lane == 0) {
-                    add_agent(&g->idle, 1u);
+                if (lane == 0)
                     __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
-                }
             }
-            // try home deque, then a random deque (3/4 same XCD, 1/4 anywhere)
+            // probe order: home, hint, then random (3/4 same XCD, 1/4 anywhere)
             uint32_t q = home;
-            if (spins & 1) {
-                uint32_t r = xorshift(rng);
-                r = __shfl(r, 0, 64);
-                if ((r & 3) != 0) q = xcc * qpx + (r >> 2) % qpx;
-                else q = (r >> 2) % pool.nq;
+            const uint32_t phase = spins % 3;
+            if (phase == 1) {
+                uint32_t hq = 0;
+                if (lane == 0) hq = ld_agent(&g->hint);
+                q = lane0(hq) % pool.nq;
+            } else if (phase == 2) {
+                uint32_t r = lane0(xorshift(rng));
+                q = ((r & 3) != 0) ? xcc * qpx + (r >> 2) % qpx : (r >> 2) % pool.nq;
             }
             uint32_t n = dequeue_chunk<Kind, CAP>(pool, q, st);
             if (n) {
@@ -240,16 +310,18 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 top = n;
                 active = true;
                 spins = 0;
-                if (lane == 0) add_agent(&g->idle, (uint32_t)-1);
+                const unsigned long long now = __builtin_amdgcn_s_memtime();
+                cyc_idle += now - t_mark;
+                t_mark = now;
                 continue;
             }
-            uint32_t outst = 0;
-            if (lane == 0) outst = ld_agent(&g->outstanding);
-            outst = __shfl(outst, 0, 64);
-            if (outst == 0) break;
-            uint32_t e = 0;
-            if (lane == 0) e = ld_agent(&g->err);
-            if (__shfl(e, 0, 64)) break;
+            uint32_t outst = 0, e = 0;
+            if (lane == 0) {
+                outst = ld_agent(&g->outstanding);
+                e = ld_agent(&g->err);
+            }
+            if (lane0(outst) == 0 || lane0(e)) break;
+            outst_pf = outst;  // fresh hunger signal for the first batch after a steal
             // bounded idle: 100 MHz constant clock, cfg.spin_limit in ms
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
             if (spins++ == 0) idle_since = now;
@@ -257,14 +329,17 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 if (lane == 0) dev_error(&g->err, kErrSpinTimeout);
                 break;
             }
-            // back off: 64*2^k cycles, capped, so idle pollers do not
-            // saturate the deque heads the working waves need
-            if (spins < 4) __builtin_amdgcn_s_sleep(1);
-            else if (spins < 16) __builtin_amdgcn_s_sleep(4);
+            // back off so idle pollers do not saturate the deque heads
+            if (spins < 8) __builtin_amdgcn_s_sleep(1);
+            else if (spins < 64) __builtin_amdgcn_s_sleep(4);
             else __builtin_amdgcn_s_sleep(16);
             continue;
         }
         ++nbatch;
+        // hunger signal: use the value loaded one batch ago (its latency hid
+        // behind that whole batch), then issue the load for the next batch
+        const uint32_t outst = lane0(outst_pf);
+        if (lane == 0) outst_pf = ld_agent(&g->outstanding);
         // ---- form a batch of up to 64 items from the top entries
         uint32_t cnt = 0, start = 0, eidx = 0;
         if ((uint32_t)lane < size) {
@@ -272,18 +347,19 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             start = st.e[eidx][W - 1];
             cnt = Kind::count(st.e[eidx]) - start;
         }
-        const int S = wave_incl_scan((int)cnt);
-        const int total = __shfl(S, 63, 64);
+        const int S = wave_scan_add((int)cnt);
+        const int total = lane63(S);
         const int take = total < kWaveSize ? total : kWaveSize;
         const int excl = S - (int)cnt;
         st.own[lane] = -1;
         __syncthreads();
         if (cnt > 0 && excl < kWaveSize) st.own[excl] = lane;
         __syncthreads();
-        const int owner = wave_incl_max_scan(st.own[lane]);
-        const int owner_excl = __shfl(excl, owner < 0 ? 0 : owner, 64);
-        const uint32_t owner_e = __shfl(eidx, owner < 0 ? 0 : owner, 64);
-        const uint32_t owner_start = __shfl(start, owner < 0 ? 0 : owner, 64);
+        const int owner = wave_scan_max(st.own[lane]);
+        const int osrc = owner < 0 ? 0 : owner;
+        const int owner_excl = __shfl(excl, osrc, 64);
+        const uint32_t owner_e = __shfl(eidx, osrc, 64);
+        const uint32_t owner_start = __shfl(start, osrc, 64);
         uint32_t out[MO][W];
         int nout = 0;
         if (lane < take) {
@@ -294,16 +370,16 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             nout = Kind::process(ctx, acc, ent, k, out, &g->err);
         }
         __syncthreads();  // every lane has read its entry before the ring changes
-        // ---- retire consumed entries (all reads of them happened above)
-        const bool full = ((uint32_t)lane < size) && S <= take;  // (0-count entries retire too)
+        // ---- retire consumed entries (0-count entries retire too)
+        const bool full = ((uint32_t)lane < size) && S <= take;
         const uint32_t nfull = __popcll(__ballot(full));
-        // entry just below the fully consumed ones may be partially consumed
+        // the entry just below the fully consumed ones may be partially consumed
         if ((uint32_t)lane == nfull && (uint32_t)lane < size && excl < take)
             st.e[eidx][W - 1] = start + (uint32_t)(take - excl);
         top -= nfull;
         // ---- push outputs
-        const int P = wave_incl_scan(nout);
-        const int tout = __shfl(P, 63, 64);
+        const int P = wave_scan_add(nout);
+        const int tout = lane63(P);
         if ((top - bot) + (uint32_t)tout > (uint32_t)CAP) {
             if (lane == 0) dev_error(&g->err, kErrStackOverflow);
             break;
@@ -316,21 +392,19 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         }
         top += (uint32_t)tout;
         __syncthreads();
-        // ---- spill the oldest entries when the ring is large, or when
-        //      some wave is idle and we hold more than spill_lo entries
+        // ---- give the oldest entries to hungry waves, or relieve a full ring
         uint32_t sz = top - bot;
-        if (sz > cfg.spill_lo) {
-            uint32_t idle = 0;
-            if (lane == 0) idle = ld_agent(&g->idle);
-            idle = __shfl(idle, 0, 64);
-            while (sz > cfg.spill_hi || (idle > 0 && sz > cfg.spill_lo)) {
-                uint32_t n = sz / 2;
+        uint32_t hungry = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
+        if (sz > cfg.spill_hi || (hungry > 0 && sz >= cfg.spill_lo)) {
+            const unsigned long long ts = __builtin_amdgcn_s_memtime();
+            while (sz > cfg.spill_hi || (hungry > 0 && sz >= cfg.spill_lo)) {
+                uint32_t n = (sz + 1) / 2;
                 if (n > pool.chunk) n = pool.chunk;
-                if (n == 0) break;
+                if (n == 0 || n == sz) break;
                 // home deque first, then the other deques of this XCD slice
                 bool ok = false;
-                for (uint32_t a = 0; a < 4 && !ok; ++a) {
-                    const uint32_t q = (a == 0) ? home : xcc * qpx + (home + a) % qpx;
+                for (uint32_t a = 0; a < qpx && !ok; ++a) {
+                    const uint32_t q = xcc * qpx + (home - xcc * qpx + a) % qpx;
                     ok = enqueue_chunk<Kind, CAP>(pool, g, q, st, bot, n);
                 }
                 if (!ok) {
@@ -342,19 +416,28 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 ++npush;
                 bot += n;
                 sz = top - bot;
-                if (idle) --idle;
+                if (hungry) --hungry;
             }
+            cyc_spill += __builtin_amdgcn_s_memtime() - ts;
         }
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        cyc_busy += now - t_mark;
+        t_mark = now;
     }
+    cyc_idle += __builtin_amdgcn_s_memtime() - t_mark;
     if (active && lane == 0) {
         // only reached on an error break: keep the protocol consistent
         __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
     }
     acc.flush(g);
     if (lane == 0) {
-        add_agent(&g->counters[13], nbatch);
-        add_agent(&g->counters[14], npush);
-        add_agent(&g->counters[15], nsteal);
+        add_agent(&g->counters[kCtrBusyCycles], cyc_busy);
+        add_agent(&g->counters[kCtrIdleCycles], cyc_idle);
+        add_agent(&g->counters[kCtrSpillCycles], cyc_spill);
+        add_agent(&g->counters[kCtrWaves], 1ull);
+        add_agent(&g->counters[kCtrBatches], nbatch);
+        add_agent(&g->counters[kCtrPushed], npush);
+        add_agent(&g->counters[kCtrStolen], nsteal);
     }
 }
 

@@ -168,7 +168,7 @@ int hclib_hip_num_cus(void) { return g_mod.inited ? g_mod.num_cus : 0; }
 
 int hclib_hip_num_workers(void) {
     if (!g_mod.inited) return 0;
-    return g_mod.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 8);
+    return g_mod.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);
 }
 
 }  // extern "C"

@@ -84,6 +84,8 @@ struct UtsCtx {
     int m;
     int shard, nshards, split;
     int hist_levels;
+    int lds_tables;  // rules/thr fit the per-wave LDS cache
+    int nthr;        // words in thr
     const int4 *rules;
     const uint32_t *thr;
     unsigned long long *hist;
@@ -180,11 +182,24 @@ struct UtsKind {
 };
 
 constexpr int kUtsCap = 512;
+constexpr size_t kUtsLdsRules = 64;       // depth rules cached in LDS per wave
+constexpr size_t kUtsLdsThr = 4 * 128;    // up to 4 GEO threshold tables
 
 __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, SchedGlobals *g,
                                                    SchedConfig cfg) {
     __shared__ WaveStack<UtsKind, kUtsCap> st;
-    run_worker<UtsKind, kUtsCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
+    __shared__ int4 s_rules[kUtsLdsRules];
+    __shared__ uint32_t s_thr[kUtsLdsThr];
+    UtsCtx c = ctx;
+    if (ctx.lds_tables) {
+        // the per-node rule lookup becomes LDS-latency (no dependent HBM/L2 loads)
+        for (int i = threadIdx.x; i < ctx.nrules; i += 64) s_rules[i] = ctx.rules[i];
+        for (int i = threadIdx.x; i < ctx.nthr; i += 64) s_thr[i] = ctx.thr[i];
+        __syncthreads();
+        c.rules = s_rules;
+        c.thr = s_thr;
+    }
+    run_worker<UtsKind, kUtsCap>(c, pool, g, cfg, st, blockIdx.x == 0);
 }
 
 // ------------------------------------------------------ host: rules/tables
@@ -437,16 +452,20 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     ctx.thr = d_thr;
     ctx.hist = max_levels ? d_hist : nullptr;
 
+    ctx.lds_tables = (T.rules.size() <= kUtsLdsRules && T.thr.size() <= kUtsLdsThr) ? 1 : 0;
+    ctx.nthr = (int)T.thr.size();
+
     PoolView pool;
     const uint32_t nq = (uint32_t)env_int("HCLIB_HIP_DEQUES", 64);
-    HX_TRY(make_pool(nq, (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
-                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 32), UtsKind::kWords, &pool));
+    HX_TRY(make_pool(nq, (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 16384),
+                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 8), UtsKind::kWords, &pool));
+    const int grid = m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);
     SchedConfig cfg;
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_SPILL_HI", 320);
     cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", 32);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
+    cfg.nwaves = (uint32_t)grid;
     HX_TRY(reset_sched(pool, 1));
-    const int grid = m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 8);
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     hipLaunchKernelGGL(k_uts_search, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
     HX_HIP(hipGetLastError());
@@ -465,9 +484,14 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     result->nodes = gl.counters[0];
     result->leaves = gl.counters[1];
     result->max_depth = gl.maxes[0];
-    result->batches = gl.counters[13];
-    result->chunks_pushed = gl.counters[14];
-    result->chunks_stolen = gl.counters[15];
+    result->batches = gl.counters[kCtrBatches];
+    result->chunks_pushed = gl.counters[kCtrPushed];
+    result->chunks_stolen = gl.counters[kCtrStolen];
     result->kernel_ms = ms;
+    const double busy = (double)gl.counters[kCtrBusyCycles],
+                 idle = (double)gl.counters[kCtrIdleCycles];
+    result->busy_frac = (busy + idle) > 0 ? busy / (busy + idle) : 0.0;
+    // s_memtime ticks at the shader clock; report with the nominal 2.4 GHz
+    result->us_per_batch = gl.counters[kCtrBatches] ? busy / gl.counters[kCtrBatches] / 2400.0 : 0.0;
     return HCLIB_HIP_OK;
 }

@@ -144,6 +144,8 @@ typedef struct {
     uint64_t chunks_stolen;  /* chunks taken from another worker's deque */
     uint64_t batches;        /* wave batches executed */
     double kernel_ms;        /* device time of the search launch (HIP events) */
+    double busy_frac;        /* share of wave time spent inside batches */
+    double us_per_batch;     /* average wave time per batch (incl. spills) */
 } hclib_hip_uts_result_t;
 
 /* Search the whole tree on the bound GPU (persistent megakernel: per-wave
@@ -173,6 +175,7 @@ typedef struct {
     uint64_t chunks_pushed;
     uint64_t chunks_stolen;
     double kernel_ms;
+    double busy_frac;        /* share of wave time spent inside batches */
 } hclib_hip_fib_result_t;
 
 /* fib(n) with one task per call and a join counter per finish scope

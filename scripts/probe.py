@@ -4,6 +4,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402,F401
 import hclib_amd as H  # noqa: E402
 
 T1 = "-t 1 -a 3 -d 10 -b 4 -r 19"
@@ -19,7 +20,8 @@ def run_uts(name, args, reps=3):
             best = r
     print(f"{name}: nodes={best['nodes']} ms={best['kernel_ms']:.3f} "
           f"Mnodes/s={best['nodes'] / best['kernel_ms'] / 1e3:.1f} batches={best['batches']} "
-          f"pushed={best['chunks_pushed']} stolen={best['chunks_stolen']}", flush=True)
+          f"pushed={best['chunks_pushed']} stolen={best['chunks_stolen']} busy={best['busy_frac']:.3f} "
+          f"us/batch={best['us_per_batch']:.2f}", flush=True)
     return best
 
 
@@ -27,10 +29,14 @@ def main():
     H.init(0)
     print("cus", H.num_cus(), flush=True)
     sweep = sys.argv[1:] if len(sys.argv) > 1 else ["base"]
+    base_env = dict(os.environ)
     for tag in sweep:
+        os.environ.clear()
+        os.environ.update(base_env)
         if tag != "base":
-            k, v = tag.split("=")
-            os.environ[k] = v
+            for kv in tag.split(","):
+                k, v = kv.split("=")
+                os.environ[k] = v
         print("== config", tag, flush=True)
         run_uts("T1", T1)
         run_uts("T3L", T3L, reps=1)
@@ -42,6 +48,8 @@ def main():
     score, st = H.sw(s1, s2, 256, 256)
     print("sw64k", score, st, flush=True)
     import torch
+    if os.environ.get("PROBE_NO_TRIAD"):
+        return
     n = 1 << 28
     b = torch.rand(n, device="cuda"); c = torch.rand(n, device="cuda"); a = torch.empty(n, device="cuda")
     s = torch.cuda.current_stream()

@@ -1,0 +1,90 @@
+/* Host-task promise semantics through include/hclib.h (no GPU needed).
+ * Restates test/c/promise/asyncAwait1.c (a chain of n asyncs, each awaiting
+ * promise i-1 and putting promise i, released by one put of promise 0),
+ * test/c/promise/future0.c (a chain of hclib_async_future) and
+ * test/c/finish1.c-style nested finish counting. Prints "Check results: OK". */
+#include <assert.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "hclib.h"
+
+static int order[64];
+static int norder = 0;
+
+static void await_fct(void *raw) {
+    void **argv = (void **)raw;
+    int index = *((int *)argv[0]);
+    hclib_future_t *f = (hclib_future_t *)argv[1];
+    hclib_promise_t *out = (hclib_promise_t *)argv[2];
+    int prev = *((int *)hclib_future_get(f));
+    assert(prev == index - 1);
+    order[norder++] = index;
+    int *v = (int *)malloc(sizeof(int));
+    *v = index;
+    hclib_promise_put(out, v);
+}
+
+static void *future_fct(void *arg) {
+    long v = (long)arg;
+    return (void *)(v + 1);
+}
+
+static int counter = 0;
+static void leaf(void *arg) { (void)arg; counter++; }
+static void spawner(void *arg) {
+    int n = *(int *)arg;
+    hclib_start_finish();
+    for (int i = 0; i < n; i++) hclib_async(leaf, NULL, NULL, 0, NULL);
+    hclib_end_finish();
+    assert(counter == n);
+}
+
+static void entrypoint(void *arg) {
+    (void)arg;
+    int n = 5;
+    hclib_promise_t **p = (hclib_promise_t **)malloc(sizeof(hclib_promise_t *) * (n + 1));
+    hclib_start_finish();
+    for (int i = 0; i <= n; i++) p[i] = hclib_promise_create();
+    for (int i = n; i >= 1; i--) {
+        void **argv = (void **)malloc(sizeof(void *) * 3);
+        argv[0] = malloc(sizeof(int));
+        *((int *)argv[0]) = i;
+        argv[1] = hclib_get_future_for_promise(p[i - 1]);
+        argv[2] = p[i];
+        hclib_future_t *fut = hclib_get_future_for_promise(p[i - 1]);
+        hclib_async(await_fct, argv, &fut, 1, NULL);
+    }
+    int *zero = (int *)malloc(sizeof(int));
+    *zero = 0;
+    hclib_promise_put(p[0], zero);
+    hclib_end_finish();
+    for (int i = 0; i < n; i++) assert(order[i] == i + 1);
+    assert(*(int *)hclib_future_get(hclib_get_future_for_promise(p[n])) == n);
+
+    /* chain of async_future, each depending on the previous */
+    hclib_future_t *f = hclib_async_future(future_fct, (void *)0L, NULL, 0, NULL);
+    for (int i = 0; i < 9; i++) {
+        long prev = (long)hclib_future_wait(f);
+        f = hclib_async_future(future_fct, (void *)prev, &f, 1, NULL);
+    }
+    assert((long)hclib_future_wait(f) == 10);
+
+    /* nested finish scopes + nonblocking end_finish */
+    int k = 7;
+    hclib_start_finish();
+    hclib_async(spawner, &k, NULL, 0, NULL);
+    hclib_end_finish();
+    hclib_start_finish();
+    hclib_async(leaf, NULL, NULL, 0, NULL);
+    hclib_future_t *done = hclib_end_finish_nonblocking();
+    hclib_future_wait(done);
+    assert(counter == k + 1);
+}
+
+int main(void) {
+    const char *deps[] = {"system"};
+    hclib_launch(entrypoint, NULL, deps, 1);
+    printf("Check results: OK\n");
+    return 0;
+}

@@ -1,0 +1,79 @@
+"""The drop-in boundary: C programs written against include/hclib.h (the
+reference's C API) compiled with gcc and linked to libhclib_amd.so.
+
+tests/c/*.c restate reference test programs (test/c/forasync1DCh.c,
+test/c/promise/asyncAwait1.c, test/c/promise/future0.c, test/fib/fib.c,
+test/uts/UTS.cpp's driver) and assert like them ("Check results: OK").
+"""
+import os
+import subprocess
+
+import pytest
+
+import hclib_amd as H
+from tests.conftest import ROOT
+
+CDIR = os.path.join(ROOT, "tests", "c")
+
+
+def _build(name, tmp_path_factory=None):
+    out = os.path.join("/tmp", f"hclib_capi_{name}_{os.getpid()}")
+    cmd = ["gcc", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"),
+           os.path.join(CDIR, name + ".c"), "-o", out, "-L", os.path.dirname(H.LIB_PATH),
+           "-lhclib_amd", "-Wl,-rpath," + os.path.dirname(H.LIB_PATH)]
+    subprocess.check_call(cmd)
+    return out
+
+
+def _run(exe, *args, timeout=300, env=None):
+    e = dict(os.environ)
+    if env:
+        e.update(env)
+    return subprocess.run([exe, *map(str, args)], capture_output=True, text=True,
+                          timeout=timeout, env=e)
+
+
+@pytest.mark.parametrize("name", ["promise_chain", "fib_gpu", "forasync1DCh_gpu", "uts_gpu"])
+def test_c_programs_compile_against_hclib_h(name):
+    assert os.path.exists(_build(name))
+
+
+def test_host_promise_semantics():
+    r = _run(_build("promise_chain"))
+    assert r.returncode == 0, r.stderr
+    assert "Check results: OK" in r.stdout
+
+
+def test_device_kinds_fail_loudly_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    r = _run(_build("fib_gpu"), 10)
+    assert r.returncode != 0
+    assert "hip module could not bind" in r.stderr
+
+
+@pytest.mark.gpu
+def test_fib_c_program_on_gpu():
+    r = _run(_build("fib_gpu"), 30)
+    assert r.returncode == 0, r.stderr
+    assert "Fib(30) = 832040 = 832040" in r.stdout and "Check results: OK" in r.stdout
+
+
+@pytest.mark.gpu
+def test_forasync1DCh_c_program_on_gpu():
+    r = _run(_build("forasync1DCh_gpu"))
+    assert r.returncode == 0, r.stderr
+    assert "Check results: OK" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["T1", "T3", "T3L"])
+def test_uts_c_program_on_gpu(golden, name):
+    g = golden("uts_goldens.json")["published"][name]
+    r = _run(_build("uts_gpu"), *g["args"].split())
+    assert r.returncode == 0, r.stderr
+    want = (f"Tree size = {g['nodes']}, tree depth = {g['depth']}, "
+            f"num leaves = {g['leaves']}")
+    assert want in r.stdout, r.stdout
