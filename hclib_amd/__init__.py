@@ -70,7 +70,7 @@ class FibResult(C.Structure):
 
 class SwResult(C.Structure):
     _fields_ = [("tiles", C.c_uint64), ("releases", C.c_uint64), ("kernel_ms", C.c_double),
-                ("cells_per_s", C.c_double)]
+                ("cells_per_s", C.c_double), ("tile_us", C.c_double), ("release_us", C.c_double)]
 
 
 # every symbol include/hclib_hip.h and include/hclib.h declare (checked by tests)
@@ -217,3 +217,10 @@ def sw_map(text: bytes) -> bytes:
     """clear_whitespaces_do_mapping (smith_waterman.cpp:45-59): keep ACGT -> 1..4."""
     table = bytes.maketrans(b"ACGT", b"\x01\x02\x03\x04")
     return bytes(x for x in text if x in b"ACGT").translate(table)
+
+
+def last_sched_counters():
+    """Counters of the last megakernel launch (see include/hclib_hip.h)."""
+    out = (C.c_uint64 * 16)()
+    lib().hclib_hip_last_sched_counters(out)
+    return list(out)

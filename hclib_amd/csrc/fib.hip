@@ -160,6 +160,7 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", 2);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
+    cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     hipLaunchKernelGGL(k_fib, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);

@@ -39,19 +39,31 @@ __device__ __forceinline__ void st4(v4f v, v4f *p) {
     else *p = v;
 }
 
-// Grid-stride tiles of 16 B per lane; UNROLL independent (b, c) pairs per
-// lane in flight; NTL / NTS select non-temporal loads / stores.
-template <bool NTL, bool NTS, int UNROLL>
-__global__ __launch_bounds__(kTriadThreads) void k_triad_f32(float *__restrict__ a,
-                                                             const float *__restrict__ b,
-                                                             const float *__restrict__ c, float s,
-                                                             int64_t n4) {
-    const int64_t stride = (int64_t)gridDim.x * kTriadThreads;
-    int64_t i = (int64_t)blockIdx.x * kTriadThreads + threadIdx.x;
+// 16 B per lane; UNROLL independent (b, c) pairs per lane in flight;
+// NTL / NTS select non-temporal loads / stores. CONTIG: each workgroup
+// streams one contiguous slice (else grid-stride interleave).
+template <bool NTL, bool NTS, int UNROLL, int THREADS, bool CONTIG>
+__global__ __launch_bounds__(THREADS) void k_triad_f32(float *__restrict__ a,
+                                                       const float *__restrict__ b,
+                                                       const float *__restrict__ c, float s,
+                                                       int64_t n4) {
+    int64_t i, end, stride;
+    if constexpr (CONTIG) {
+        const int64_t q = (int64_t)THREADS * UNROLL;
+        const int64_t span = ((n4 + gridDim.x - 1) / gridDim.x + q - 1) / q * q;
+        i = (int64_t)blockIdx.x * span + threadIdx.x;
+        end = (int64_t)blockIdx.x * span + span;
+        if (end > n4) end = n4;
+        stride = THREADS;
+    } else {
+        i = (int64_t)blockIdx.x * THREADS + threadIdx.x;
+        end = n4;
+        stride = (int64_t)gridDim.x * THREADS;
+    }
     const v4f *b4 = reinterpret_cast<const v4f *>(b);
     const v4f *c4 = reinterpret_cast<const v4f *>(c);
     v4f *a4 = reinterpret_cast<v4f *>(a);
-    for (; i + (UNROLL - 1) * stride < n4; i += UNROLL * stride) {
+    for (; i + (UNROLL - 1) * stride < end; i += UNROLL * stride) {
         v4f vb[UNROLL], vc[UNROLL];
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
@@ -68,7 +80,7 @@ __global__ __launch_bounds__(kTriadThreads) void k_triad_f32(float *__restrict__
             st4<NTS>(r, &a4[i + u * stride]);
         }
     }
-    for (; i < n4; i += stride) {
+    for (; i < end; i += stride) {
         v4f vb = ld4<NTL>(&b4[i]), vc = ld4<NTL>(&c4[i]), r;
         r.x = triad1(vb.x, vc.x, s);
         r.y = triad1(vb.y, vc.y, s);
@@ -79,18 +91,30 @@ __global__ __launch_bounds__(kTriadThreads) void k_triad_f32(float *__restrict__
 }
 
 typedef void (*triad_kernel_t)(float *, const float *, const float *, float, int64_t);
-// variant bits: 1 = nt loads, 2 = nt stores, 4 = unroll 8 (else 4)
-static triad_kernel_t triad_variant(int v) {
+
+template <int THREADS, bool CONTIG>
+static triad_kernel_t triad_pick(int v) {
     switch (v & 7) {
-    case 0: return k_triad_f32<false, false, 4>;
-    case 1: return k_triad_f32<true, false, 4>;
-    case 2: return k_triad_f32<false, true, 4>;
-    case 3: return k_triad_f32<true, true, 4>;
-    case 4: return k_triad_f32<false, false, 8>;
-    case 5: return k_triad_f32<true, false, 8>;
-    case 6: return k_triad_f32<false, true, 8>;
-    default: return k_triad_f32<true, true, 8>;
+    case 0: return k_triad_f32<false, false, 4, THREADS, CONTIG>;
+    case 1: return k_triad_f32<true, false, 4, THREADS, CONTIG>;
+    case 2: return k_triad_f32<false, true, 4, THREADS, CONTIG>;
+    case 3: return k_triad_f32<true, true, 4, THREADS, CONTIG>;
+    case 4: return k_triad_f32<false, false, 8, THREADS, CONTIG>;
+    case 5: return k_triad_f32<true, false, 8, THREADS, CONTIG>;
+    case 6: return k_triad_f32<false, true, 8, THREADS, CONTIG>;
+    default: return k_triad_f32<true, true, 8, THREADS, CONTIG>;
     }
+}
+
+// variant bits: 1 = nt loads, 2 = nt stores, 4 = unroll 8 (else 4),
+// 8 = contiguous slice per workgroup, 16/32 = 512/1024 threads (else 256)
+static triad_kernel_t triad_variant(int v, int *threads) {
+    const bool contig = (v & 8) != 0;
+    const int t = (v >> 4) & 3;
+    *threads = t == 1 ? 512 : (t == 2 ? 1024 : 256);
+    if (t == 1) return contig ? triad_pick<512, true>(v) : triad_pick<512, false>(v);
+    if (t == 2) return contig ? triad_pick<1024, true>(v) : triad_pick<1024, false>(v);
+    return contig ? triad_pick<256, true>(v) : triad_pick<256, false>(v);
 }
 
 __global__ void k_triad_tail(float *a, const float *b, const float *c, float s, int64_t from,
@@ -235,12 +259,15 @@ extern "C" int hclib_hip_forasync_triad_f32(float *a, const float *b, const floa
     }
     const int64_t n4 = n / 4;
     if (n4 > 0) {
-        const int bpc = env_int("HCLIB_HIP_TRIAD_BLOCKS_PER_CU", 2);
+        // measured best on MI355X (scripts/probe_triad.py): one 256-thread
+        // workgroup per CU, non-temporal loads + stores, 4 pairs in flight
+        const int bpc = env_int("HCLIB_HIP_TRIAD_BLOCKS_PER_CU", 1);
+        int threads = kTriadThreads;
+        triad_kernel_t k = triad_variant(env_int("HCLIB_HIP_TRIAD_VARIANT", 3), &threads);
         int64_t grid = (int64_t)mod().num_cus * bpc;
-        const int64_t need = (n4 + kTriadThreads - 1) / kTriadThreads;
+        const int64_t need = (n4 + threads - 1) / threads;
         if (grid > need) grid = need;
-        hipLaunchKernelGGL(triad_variant(env_int("HCLIB_HIP_TRIAD_VARIANT", 7)),
-                           dim3((unsigned)grid), dim3(kTriadThreads), 0, st, a, b, c, s, n4);
+        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(threads), 0, st, a, b, c, s, n4);
         HX_HIP(hipGetLastError());
     }
     if (n4 * 4 < n) {

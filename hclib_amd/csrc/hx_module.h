@@ -24,6 +24,7 @@ struct Module {
     void *pool_mem = nullptr;
     size_t pool_bytes = 0;
     SchedGlobals *globals = nullptr;
+    unsigned long long last_counters[16] = {};  // counters of the last megakernel launch
 };
 
 Module &mod();

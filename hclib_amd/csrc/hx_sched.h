@@ -59,6 +59,8 @@ struct alignas(256) SchedGlobals {
 
 // scheduler counters (SchedGlobals::counters)
 enum : int {
+    kCtrFormCycles = 7,   // diagnostic stamps: batch formation (scans, LDS map)
+    kCtrProcCycles = 8,   // diagnostic stamps: Kind::process over the batch
     kCtrBusyCycles = 9,   // s_memtime cycles inside batches (all waves)
     kCtrIdleCycles = 10,  // s_memtime cycles idle / stealing
     kCtrSpillCycles = 11, // cycles inside enqueue
@@ -83,6 +85,7 @@ struct SchedConfig {
     uint32_t spill_lo;   // give away entries to hungry waves when holding >= this many
     uint32_t spin_limit; // ms a wave may stay idle before declaring a timeout
     uint32_t nwaves;     // waves in the launch (hunger = nwaves - outstanding)
+    uint32_t stamps;     // diagnostic: accumulate per-phase s_memtime cycles
 };
 
 // Kind concept:
@@ -162,27 +165,31 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
     uint32_t pos = 0;
     int ok = 0;
     if (lane == 0) {
-        pos = ld_agent(&h->tail);
-        for (int it = 0; it < 64; ++it) {
-            uint32_t s = ld_agent(&pool.seq[q * pool.cap + (pos & (pool.cap - 1))]);
-            int dif = (int)(s - pos);
-            if (dif == 0) {
-                if (cas_agent(&h->tail, pos, pos + 1)) { ok = 1; break; }
-                pos = ld_agent(&h->tail);
-            } else if (dif < 0) {
-                break;  // full
-            } else {
-                pos = ld_agent(&h->tail);
-            }
+        // a producer takes a ticket with ONE fetch-add (no CAS retry storms);
+        // it only does so while the ring is at most half full, so a ticket
+        // never waits behind a consumer that cannot come
+        const uint32_t hd = ld_agent(&h->head), tl = ld_agent(&h->tail);
+        if ((int)(tl - hd) < (int)(pool.cap / 2)) {
+            add_agent(&g->outstanding, 1u);  // counts before it becomes visible
+            pos = add_agent(&h->tail, 1u);
+            ok = 1;
         }
     }
-    ok = __shfl(ok, 0, 64);
-    if (!ok) return false;
-    pos = __shfl(pos, 0, 64);
+    if (!lane0((uint32_t)ok)) return false;
+    pos = lane0(pos);
     const uint32_t slot = q * pool.cap + (pos & (pool.cap - 1));
+    if (lane == 0) {
+        // the slot is free once its previous lap was consumed (normally at once)
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (ld_agent(&pool.seq[slot]) != pos) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s
+                dev_error(&g->err, kErrQueueFull);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
     uint32_t *dst = pool.data + (size_t)slot * pool.chunk * W;
-    // the reservation counts as outstanding work before it becomes visible
-    if (lane == 0) add_agent(&g->outstanding, 1u);
     for (uint32_t i = lane; i < n * W; i += kWaveSize) {
         uint32_t ent = i / W, w = i % W;
         st_agent(&dst[i], st.e[(bot + ent) & (CAP - 1)][w]);
@@ -199,32 +206,36 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
 // Try to take one chunk from deque q into the (empty) stack. Returns the
 // number of entries taken (0 if the deque looked empty).
 template <class Kind, int CAP>
-__device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Kind, CAP> &st) {
+__device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Kind, CAP> &st,
+                                  SchedGlobals *g) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     QueueHdr *h = &pool.hdr[q];
     uint32_t pos = 0;
     int ok = 0;
     if (lane == 0) {
-        pos = ld_agent(&h->head);
-        for (int it = 0; it < 16; ++it) {
-            uint32_t s = ld_agent(&pool.seq[q * pool.cap + (pos & (pool.cap - 1))]);
-            int dif = (int)(s - (pos + 1));
-            if (dif == 0) {
-                if (cas_agent(&h->head, pos, pos + 1)) { ok = 1; break; }
-                pos = ld_agent(&h->head);
-            } else if (dif < 0) {
-                break;  // empty (or the producer has not published yet)
-            } else {
-                pos = ld_agent(&h->head);
-            }
+        // one claim attempt: a ticket below the tail, taken by CAS on the head
+        const uint32_t hd = ld_agent(&h->head), tl = ld_agent(&h->tail);
+        if ((int)(tl - hd) > 0 && cas_agent(&h->head, hd, hd + 1)) {
+            pos = hd;
+            ok = 1;
         }
     }
-    ok = __shfl(ok, 0, 64);
-    if (!ok) return 0;
-    pos = __shfl(pos, 0, 64);
-    handoff_consume();
+    if (!lane0((uint32_t)ok)) return 0;
+    pos = lane0(pos);
     const uint32_t slot = q * pool.cap + (pos & (pool.cap - 1));
+    if (lane == 0) {
+        // the producer holds this ticket and is publishing it (bounded wait)
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (ld_agent(&pool.seq[slot]) != pos + 1) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s
+                dev_error(&g->err, kErrSpinTimeout);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    handoff_consume();
     const uint32_t n = ld_agent(&pool.cnt[slot]);
     const uint32_t *src = pool.data + (size_t)slot * pool.chunk * W;
     for (uint32_t i = lane; i < n * W; i += kWaveSize) {
@@ -264,7 +275,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     uint32_t spins = 0;
     unsigned long long idle_since = 0;
     unsigned long long nbatch = 0, npush = 0, nsteal = 0;
-    unsigned long long cyc_busy = 0, cyc_idle = 0, cyc_spill = 0;
+    unsigned long long cyc_busy = 0, cyc_idle = 0, cyc_spill = 0, cyc_form = 0, cyc_proc = 0;
 
     if (seed_roots) {
         uint32_t out[MO > 4 ? MO : 4][W];
@@ -303,7 +314,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 uint32_t r = lane0(xorshift(rng));
                 q = ((r & 3) != 0) ? xcc * qpx + (r >> 2) % qpx : (r >> 2) % pool.nq;
             }
-            uint32_t n = dequeue_chunk<Kind, CAP>(pool, q, st);
+            uint32_t n = dequeue_chunk<Kind, CAP>(pool, q, st, g);
             if (n) {
                 if (q != home) ++nsteal;
                 bot = 0;
@@ -355,19 +366,28 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         __syncthreads();
         if (cnt > 0 && excl < kWaveSize) st.own[excl] = lane;
         __syncthreads();
-        const int owner = wave_scan_max(st.own[lane]);
-        const int osrc = owner < 0 ? 0 : owner;
-        const int owner_excl = __shfl(excl, osrc, 64);
-        const uint32_t owner_e = __shfl(eidx, osrc, 64);
-        const uint32_t owner_start = __shfl(start, osrc, 64);
+        // item `lane` belongs to the last entry whose first item is <= lane:
+        // two DPP max-scans give that entry and where its items start
+        const int mark = st.own[lane];
+        const int owner = wave_scan_max(mark);
+        const int owner_excl = wave_scan_max(mark >= 0 ? lane : -1);
+        const uint32_t owner_e = (top - 1 - (uint32_t)(owner < 0 ? 0 : owner)) & (CAP - 1);
         uint32_t out[MO][W];
         int nout = 0;
+        unsigned long long ts0 = 0;
+        if (cfg.stamps) ts0 = __builtin_amdgcn_s_memtime();
         if (lane < take) {
             uint32_t ent[W];
 #pragma unroll
             for (int w = 0; w < W; ++w) ent[w] = st.e[owner_e][w];
-            const uint32_t k = owner_start + (uint32_t)(lane - owner_excl);
+            const uint32_t k = ent[W - 1] + (uint32_t)(lane - owner_excl);
             nout = Kind::process(ctx, acc, ent, k, out, &g->err);
+        }
+        if (cfg.stamps) {
+            // diagnostic build only: wait for the lanes' work, then stamp
+            const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+            cyc_form += ts0 - t_mark;
+            cyc_proc += ts1 - ts0;
         }
         __syncthreads();  // every lane has read its entry before the ring changes
         // ---- retire consumed entries (0-count entries retire too)
@@ -432,6 +452,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     acc.flush(g);
     if (lane == 0) {
         add_agent(&g->counters[kCtrBusyCycles], cyc_busy);
+        if (cfg.stamps) {
+            add_agent(&g->counters[kCtrFormCycles], cyc_form);
+            add_agent(&g->counters[kCtrProcCycles], cyc_proc);
+        }
         add_agent(&g->counters[kCtrIdleCycles], cyc_idle);
         add_agent(&g->counters[kCtrSpillCycles], cyc_spill);
         add_agent(&g->counters[kCtrWaves], 1ull);

@@ -104,6 +104,7 @@ int finish_sched(SchedGlobals *host_copy, const char *who) {
     HX_HIP(hipMemcpyAsync(host_copy, m.globals, sizeof(SchedGlobals), hipMemcpyDeviceToHost,
                           m.stream));
     HX_HIP(hipStreamSynchronize(m.stream));
+    memcpy(m.last_counters, host_copy->counters, sizeof(m.last_counters));
     if (host_copy->err) {
         set_error("%s: device error %u (%s)", who, host_copy->err, err_name(host_copy->err));
         return HCLIB_HIP_EDEVICE;
@@ -165,6 +166,10 @@ void hclib_hip_finalize(void) {
 }
 
 int hclib_hip_num_cus(void) { return g_mod.inited ? g_mod.num_cus : 0; }
+
+void hclib_hip_last_sched_counters(uint64_t out[16]) {
+    for (int i = 0; i < 16; ++i) out[i] = g_mod.last_counters[i];
+}
 
 int hclib_hip_num_workers(void) {
     if (!g_mod.inited) return 0;

@@ -56,8 +56,9 @@ __device__ __forceinline__ int sw_m(uint32_t row, int b) {
 }
 
 __device__ __forceinline__ int shift_up1(int v) {
-    // lane L receives lane L-1's value (lane 0 receives garbage; it reads LDS)
-    return __shfl_up(v, 1, 64);
+    // lane L receives lane L-1's value in one DPP move (GFX9 wave_shr:1);
+    // lane 0 receives 0 and reads its input from LDS instead
+    return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
 }
 
 __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, int8_t *lds_s1) {
@@ -104,14 +105,21 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
         if (lane == last_lane) lds_bot[0] = left[last_q];  // H[band last row][0]
         int out = 0;
         const int steps = tw + 63;
+        // LDS operands of step s are loaded during step s-1 (latency hidden)
+        int c0 = -lane < 0 ? 0 : -lane;
+        int b_cur = lds_s1[c0], top_cur = lds_top[c0 + 1];
         for (int s = 0; s < steps; ++s) {
             const int recv = shift_up1(out);
             const int cidx = s - lane;  // 0-based column
+            int cn = cidx + 1;
+            cn = cn < 0 ? 0 : (cn >= tw ? tw - 1 : cn);
+            const int b_nxt = lds_s1[cn];
+            const int top_nxt = lds_top[cn + 1];
             if (cidx >= 0 && cidx < tw && nvalid > 0) {
-                int up = (lane == 0) ? lds_top[cidx + 1] : recv;
+                int up = (lane == 0) ? top_cur : recv;
                 int diag = up_prev;
                 up_prev = up;
-                const int b = lds_s1[cidx];
+                const int b = b_cur;
 #pragma unroll
                 for (int q = 0; q < kSwRP; ++q) {
                     const int dsc = diag + sw_m(mrow[q], b);
@@ -131,6 +139,8 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
                         if (q < nvalid) st_agent(&c.right[(size_t)t * th + rfirst + q], left[q]);
                 }
             }
+            b_cur = b_nxt;
+            top_cur = top_nxt;
         }
         __syncthreads();
         // the band's bottom row becomes the next band's top row
@@ -148,7 +158,7 @@ __global__ __launch_bounds__(64) void k_sw(SwCtx c) {
     int8_t *lds_s1 = (int8_t *)(lds_bot + ((c.tw + 1 + 3) & ~3));
     const int lane = lane_id();
     const uint32_t ntiles = (uint32_t)(c.ntw * c.nth);
-    unsigned long long ntile = 0, nrel = 0;
+    unsigned long long ntile = 0, nrel = 0, cyc_tile = 0, cyc_rel = 0;
     while (true) {
         uint32_t ticket = 0;
         if (lane == 0) ticket = add_agent(c.ready_head, 1u);
@@ -168,31 +178,41 @@ __global__ __launch_bounds__(64) void k_sw(SwCtx c) {
         }
         t = __shfl(t, 0, 64);
         if (t == kEmpty) break;
-        acquire_agent();
+        // inputs are read with sc1 loads only: no L1 invalidate needed
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
         sw_tile(c, t, lds_top, lds_bot, lds_s1);
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        cyc_tile += t1 - t0;
         ++ntile;
-        release_agent();  // every store of this tile drained and released
+        // every output word was stored write-through (sc1); drain them before
+        // the counters that publish the tile (MI355X_MICROARCH.md, Valid forms:
+        // sc1 payload + drained counter; consumers read with sc1 loads)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) {
             const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
-            const uint32_t succ[3] = {t + 1, t + (uint32_t)c.ntw, t + (uint32_t)c.ntw + 1};
-            const bool ok[3] = {j + 1 < c.ntw, i + 1 < c.nth, j + 1 < c.ntw && i + 1 < c.nth};
+#pragma unroll
             for (int k = 0; k < 3; ++k) {
-                if (!ok[k]) continue;
+                const uint32_t succ = k == 0 ? t + 1 : (k == 1 ? t + (uint32_t)c.ntw : t + (uint32_t)c.ntw + 1);
+                const bool ok = k == 0 ? (j + 1 < c.ntw) : (k == 1 ? (i + 1 < c.nth) : (j + 1 < c.ntw && i + 1 < c.nth));
+                if (!ok) continue;
                 ++nrel;
-                const uint32_t old = __hip_atomic_fetch_add(&c.deps[succ[k]], (uint32_t)-1,
-                                                            __ATOMIC_ACQ_REL, HX_AGENT);
+                const uint32_t old = add_agent(&c.deps[succ], (uint32_t)-1);
                 if (old == 1) {
                     const uint32_t pos = add_agent(c.ready_tail, 1u);
-                    __hip_atomic_store(&c.ready[pos], succ[k], __ATOMIC_RELEASE, HX_AGENT);
+                    st_agent(&c.ready[pos], succ);
                 }
             }
         }
         __syncthreads();
+        cyc_rel += __builtin_amdgcn_s_memtime() - t1;
     }
     if (lane == 0) {
         add_agent(&c.stats[0], ntile);
         add_agent(&c.stats[1], nrel);
+        add_agent(&c.stats[2], cyc_tile);
+        add_agent(&c.stats[3], cyc_rel);
     }
 }
 
@@ -281,11 +301,11 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     if ((rc = hip_check(hipGetLastError(), "k_sw launch"))) return fail(rc);
     if ((rc = hip_check(hipEventRecord(m.ev1, m.stream), "event"))) return fail(rc);
     uint32_t herr = 0;
-    unsigned long long st[2] = {0, 0};
+    unsigned long long st[4] = {0, 0, 0, 0};
     int corner = 0;
     if ((rc = hip_check(hipStreamSynchronize(m.stream), "k_sw"))) return fail(rc);
     (void)hipMemcpy(&herr, c.err, 4, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(st, c.stats, 16, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(st, c.stats, 32, hipMemcpyDeviceToHost);
     (void)hipMemcpy(&corner, c.corner + (nt - 1), 4, hipMemcpyDeviceToHost);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
@@ -304,6 +324,8 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         result->releases = st[1];
         result->kernel_ms = ms;
         result->cells_per_s = (double)nt * tw * th / (ms * 1e-3);
+        result->tile_us = st[0] ? (double)st[2] / st[0] / 2400.0 : 0.0;
+        result->release_us = st[0] ? (double)st[3] / st[0] / 2400.0 : 0.0;
     }
     return HCLIB_HIP_OK;
 }

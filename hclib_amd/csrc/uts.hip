@@ -462,9 +462,10 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     const int grid = m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);
     SchedConfig cfg;
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_SPILL_HI", 320);
-    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", 32);
+    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", 24);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
+    cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     hipLaunchKernelGGL(k_uts_search, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);

@@ -64,6 +64,11 @@ const char *hclib_hip_last_error(void);
 int hclib_hip_num_cus(void);
 /* Module version string, also proves the library loads without a GPU. */
 const char *hclib_hip_version(void);
+/* Scheduler counters of the last megakernel launch (HCLIB_STATS analogue,
+ * src/hclib-runtime.c:83-104): [0..1] kind totals, [7..8] diagnostic phase
+ * cycles (HCLIB_HIP_STAMPS=1), [9] busy, [10] idle, [11] spill cycles,
+ * [12] waves, [13] batches, [14] chunks pushed, [15] chunks stolen. */
+void hclib_hip_last_sched_counters(uint64_t out[16]);
 
 /* ------------------------------------------------------------ forasync */
 /* hclib_loop_domain_t of inc/hclib-task.h:53-58 (int bounds, 16 bytes). */
@@ -188,6 +193,8 @@ typedef struct {
     uint64_t releases;   /* dependency-counter decrements */
     double kernel_ms;
     double cells_per_s;
+    double tile_us;      /* average in-tile DP time per tile task */
+    double release_us;   /* average dependency-release time per tile task */
 } hclib_hip_sw_result_t;
 
 /* Tiled global alignment of smith_waterman.cpp over host sequences coded

@@ -11,8 +11,11 @@ n = 1 << 28
 b = torch.rand(n, device="cuda"); c = torch.rand(n, device="cuda"); a = torch.empty(n, device="cuda")
 s = torch.cuda.current_stream()
 exp = torch.add(b, torch.mul(c, 3.0))
-for var in range(8):
-    for bpc in (2, 4, 8, 16, 32):
+import itertools
+VARS = [int(x) for x in os.environ.get("TRIAD_VARS", "7,3,15,11,23,31,39,47").split(",")]
+BPCS = [int(x) for x in os.environ.get("TRIAD_BPCS", "1,2,4").split(",")]
+for var, bpc in itertools.product(VARS, BPCS):
+    if True:
         os.environ["HCLIB_HIP_TRIAD_VARIANT"] = str(var)
         os.environ["HCLIB_HIP_TRIAD_BLOCKS_PER_CU"] = str(bpc)
         for _ in range(3):
