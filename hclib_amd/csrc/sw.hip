@@ -45,14 +45,11 @@ struct SwCtx {
     uint32_t spin_ms;
 };
 
-// alignment_score_matrix (smith_waterman.cpp:36-43) row for s2 code a,
-// packed as four signed bytes for s1 = 1..4
-__device__ __forceinline__ uint32_t sw_row(int a) {
-    // A: 2 -4 -2 -4 | C: -4 2 -4 -2 | G: -2 -4 2 -4 | T: -4 -2 -4 2
-    return a == 1 ? 0xfcfefc02u : a == 2 ? 0xfefc02fcu : a == 3 ? 0xfc02fcfeu : 0x02fcfefcu;
-}
-__device__ __forceinline__ int sw_m(uint32_t row, int b) {
-    return (int)(int8_t)(row >> (8 * (b - 1)));
+// alignment_score_matrix (smith_waterman.cpp:36-43) row for s2 code a, plus
+// 2 (see the G transform below), packed as four signed bytes for s1 = 1..4:
+// A: 4 -2 0 -2 | C: -2 4 -2 0 | G: 0 -2 4 -2 | T: -2 0 -2 4
+__device__ __forceinline__ uint32_t sw_row2(int a) {
+    return a == 1 ? 0xfe00fe04u : a == 2 ? 0x00fe04feu : a == 3 ? 0xfe04fe00u : 0x04fe00feu;
 }
 
 __device__ __forceinline__ int shift_up1(int v) {
@@ -61,21 +58,30 @@ __device__ __forceinline__ int shift_up1(int v) {
     return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
 }
 
+// One tile task. The DP runs on G = H + row + col (matrix indices): with the
+// unit gap penalty, H = max(H_left - 1, H_up - 1, H_diag + M) becomes
+// G = max3(G_left, G_up, G_diag + M + 2) — one dependent max3 per cell.
+// Inputs are converted to G when loaded, outputs back to H when stored, so
+// the promises' data (bottom row, right column, corner) are the reference's.
 __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, int8_t *lds_s1) {
     const int lane = lane_id();
     const int i = (int)(t / (uint32_t)c.ntw) + 1;  // tile row (1-based)
     const int j = (int)(t % (uint32_t)c.ntw) + 1;  // tile col
     const int tw = c.tw, th = c.th;
+    const int R0 = (i - 1) * th + 1, C0 = (j - 1) * tw + 1;  // matrix index of cell (0,0)
     const uint32_t tup = t - (uint32_t)c.ntw, tleft = t - 1, tdiag = t - (uint32_t)c.ntw - 1;
     // s1 segment of this tile column
     for (int q = lane; q < tw; q += 64) lds_s1[q] = c.s1[(size_t)(j - 1) * tw + q];
-    // top row (row -1 of the tile, columns 0..tw): corner + above tile bottom row
+    // top row = matrix row R0-1, columns C0-1 .. C0-1+tw: corner + above tile's bottom row
     if (lane == 0) {
-        lds_top[0] = (i == 1) ? -((j - 1) * tw) : (j == 1 ? -((i - 1) * th) : ld_agent(&c.corner[tdiag]));
-        if (i == 1 && j == 1) lds_top[0] = 0;
+        int h = (i == 1) ? -((j - 1) * tw) : (j == 1 ? -((i - 1) * th) : ld_agent(&c.corner[tdiag]));
+        if (i == 1 && j == 1) h = 0;
+        lds_top[0] = h + (R0 - 1) + (C0 - 1);
     }
-    for (int q = lane; q < tw; q += 64)
-        lds_top[q + 1] = (i == 1) ? -((j - 1) * tw + q + 1) : ld_agent(&c.bottom[(size_t)tup * tw + q]);
+    for (int q = lane; q < tw; q += 64) {
+        const int h = (i == 1) ? -((j - 1) * tw + q + 1) : ld_agent(&c.bottom[(size_t)tup * tw + q]);
+        lds_top[q + 1] = h + (R0 - 1) + (C0 + q);
+    }
     __syncthreads();
     for (int r0 = 0; r0 < th; r0 += 64 * kSwRP) {
         const int rfirst = r0 + lane * kSwRP;
@@ -87,28 +93,47 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
             const int r = rfirst + q;
             if (r < th) {
                 ++nvalid;
-                left[q] = (j == 1) ? -((i - 1) * th + r + 1) : ld_agent(&c.right[(size_t)tleft * th + r]);
-                mrow[q] = sw_row(c.s2[(size_t)(i - 1) * th + r]);
+                const int h = (j == 1) ? -((i - 1) * th + r + 1) : ld_agent(&c.right[(size_t)tleft * th + r]);
+                left[q] = h + (R0 + r) + (C0 - 1);
+                mrow[q] = sw_row2(c.s2[(size_t)(i - 1) * th + r]);
             } else {
                 left[q] = 0;
                 mrow[q] = 0;
             }
         }
-        // H[rfirst-1][0]: the left boundary one row up (corner for row 0)
+        // G at (rfirst-1, column 0): the left boundary one row up (corner for row 0)
         int up_prev;
         if (rfirst == 0) up_prev = lds_top[0];
-        else if (j == 1) up_prev = -((i - 1) * th + rfirst);
-        else up_prev = (rfirst - 1 < th) ? ld_agent(&c.right[(size_t)tleft * th + rfirst - 1]) : 0;
+        else if (j == 1) up_prev = -((i - 1) * th + rfirst) + (R0 + rfirst - 1) + (C0 - 1);
+        else up_prev = (rfirst - 1 < th)
+                           ? ld_agent(&c.right[(size_t)tleft * th + rfirst - 1]) + (R0 + rfirst - 1) + (C0 - 1)
+                           : 0;
         const int band_rows = (th - r0) < 64 * kSwRP ? (th - r0) : 64 * kSwRP;
         const int last_lane = (band_rows - 1) / kSwRP;
         const int last_q = (band_rows - 1) % kSwRP;
-        if (lane == last_lane) lds_bot[0] = left[last_q];  // H[band last row][0]
+        if (lane == last_lane) lds_bot[0] = left[last_q];  // G[band last row][0]
         int out = 0;
         const int steps = tw + 63;
         // LDS operands of step s are loaded during step s-1 (latency hidden)
         int c0 = -lane < 0 ? 0 : -lane;
         int b_cur = lds_s1[c0], top_cur = lds_top[c0 + 1];
-        for (int s = 0; s < steps; ++s) {
+        // one anti-diagonal step of this lane's kSwRP rows
+        auto cell_rows = [&](int up) {
+            int diag = up_prev;
+            up_prev = up;
+            const int sh = (b_cur << 3) - 8;  // byte of the s1 code in the packed score row
+#pragma unroll
+            for (int q = 0; q < kSwRP; ++q) {
+                const int d = diag + __builtin_amdgcn_sbfe((int)mrow[q], sh, 8);
+                const int a = left[q] > up ? left[q] : up;
+                const int h = a > d ? a : d;
+                diag = left[q];
+                left[q] = h;
+                up = h;
+            }
+            return up;
+        };
+        auto masked_step = [&](int s) {
             const int recv = shift_up1(out);
             const int cidx = s - lane;  // 0-based column
             int cn = cidx + 1;
@@ -116,46 +141,54 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
             const int b_nxt = lds_s1[cn];
             const int top_nxt = lds_top[cn + 1];
             if (cidx >= 0 && cidx < tw && nvalid > 0) {
-                int up = (lane == 0) ? top_cur : recv;
-                int diag = up_prev;
-                up_prev = up;
-                const int b = b_cur;
-#pragma unroll
-                for (int q = 0; q < kSwRP; ++q) {
-                    const int dsc = diag + sw_m(mrow[q], b);
-                    const int l = left[q] - 1;
-                    const int u = up - 1;
-                    const int lt = l > u ? l : u;
-                    const int h = lt > dsc ? lt : dsc;
-                    diag = left[q];
-                    left[q] = h;
-                    up = h;
-                }
-                out = up;
+                out = cell_rows((lane == 0) ? top_cur : recv);
                 if (lane == last_lane) lds_bot[cidx + 1] = left[last_q];
-                if (cidx == tw - 1) {
-#pragma unroll
-                    for (int q = 0; q < kSwRP; ++q)
-                        if (q < nvalid) st_agent(&c.right[(size_t)t * th + rfirst + q], left[q]);
-                }
             }
             b_cur = b_nxt;
             top_cur = top_nxt;
+        };
+        int s = 0;
+        if (band_rows == 64 * kSwRP && tw > 64) {
+            // ramp-in, a branch-free steady state in which every lane is on a
+            // valid column (s-63 .. s), then ramp-out
+            for (; s < 63; ++s) masked_step(s);
+            const int dummy = tw + 2 + lane;  // lds_bot has 64 spare words past tw+1
+            for (; s < tw; ++s) {
+                const int recv = shift_up1(out);
+                const int cidx = s - lane;
+                const int cn = cidx + 1 < tw ? cidx + 1 : tw - 1;
+                const int b_nxt = lds_s1[cn];
+                const int top_nxt = lds_top[cn + 1];
+                out = cell_rows(lane == 0 ? top_cur : recv);
+                // lane 63 owns the band's last row; the others hit a private dummy word
+                lds_bot[(lane == 63) ? cidx + 1 : dummy] = out;
+                b_cur = b_nxt;
+                top_cur = top_nxt;
+            }
         }
+        for (; s < steps; ++s) masked_step(s);
+        // the right column H[row][tw] is each lane's final `left`
+#pragma unroll
+        for (int q = 0; q < kSwRP; ++q)
+            if (q < nvalid)
+                st_agent(&c.right[(size_t)t * th + rfirst + q],
+                         left[q] - (R0 + rfirst + q) - (C0 + tw - 1));
         __syncthreads();
-        // the band's bottom row becomes the next band's top row
+        // the band's bottom row becomes the next band's top row (both in G)
         for (int q = lane; q <= tw; q += 64) lds_top[q] = lds_bot[q];
         __syncthreads();
     }
-    for (int q = lane; q < tw; q += 64) st_agent(&c.bottom[(size_t)t * tw + q], lds_top[q + 1]);
-    if (lane == 0) st_agent(&c.corner[t], lds_top[tw]);
+    const int Rb = R0 + th - 1;  // matrix row of the tile's bottom row
+    for (int q = lane; q < tw; q += 64)
+        st_agent(&c.bottom[(size_t)t * tw + q], lds_top[q + 1] - Rb - (C0 + q));
+    if (lane == 0) st_agent(&c.corner[t], lds_top[tw] - Rb - (C0 + tw - 1));
 }
 
 __global__ __launch_bounds__(64) void k_sw(SwCtx c) {
     extern __shared__ __attribute__((aligned(16))) int sw_lds[];
     int *lds_top = sw_lds;
     int *lds_bot = sw_lds + ((c.tw + 1 + 3) & ~3);
-    int8_t *lds_s1 = (int8_t *)(lds_bot + ((c.tw + 1 + 3) & ~3));
+    int8_t *lds_s1 = (int8_t *)(lds_bot + ((c.tw + 1 + 3) & ~3) + 68);  // + 64 dummy words
     const int lane = lane_id();
     const uint32_t ntiles = (uint32_t)(c.ntw * c.nth);
     unsigned long long ntile = 0, nrel = 0, cyc_tile = 0, cyc_rel = 0;
@@ -287,10 +320,10 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         if ((rc = hip_check(hipMemcpyAsync(c.ready_tail, &one, 4, hipMemcpyHostToDevice, m.stream), "tail"))) return fail(rc);
     }
     hipLaunchKernelGGL(k_sw_init, dim3(1024), dim3(256), 0, m.stream, c.deps, c.ready, c.ntw, c.nth);
-    const size_t lds = 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + (size_t)tw + 16;
+    const size_t lds = 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + 68 * 4 + (size_t)tw + 16;
     if (lds > 160 * 1024) return fail((set_error("hclib_hip_sw: tile width too large for LDS"), HCLIB_HIP_EINVAL));
     int per_cu = (int)((160 * 1024) / lds);
-    int wpc = env_int("HCLIB_HIP_SW_WAVES_PER_CU", 8);
+    int wpc = env_int("HCLIB_HIP_SW_WAVES_PER_CU", 2);
     if (wpc > per_cu) wpc = per_cu;
     if (wpc < 1) wpc = 1;
     const int grid = m.num_cus * wpc;
