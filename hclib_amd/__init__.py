@@ -78,7 +78,7 @@ EXPORTS_HIP = [
     "hclib_hip_init", "hclib_hip_finalize", "hclib_hip_last_error", "hclib_hip_num_cus",
     "hclib_hip_version", "hclib_hip_forasync", "hclib_hip_forasync_triad_f32",
     "hclib_hip_num_workers", "hclib_hip_uts_search", "hclib_hip_uts_num_children_host",
-    "hclib_hip_fib", "hclib_hip_sw",
+    "hclib_hip_fib", "hclib_hip_sw", "hclib_hip_last_sched_counters",
 ]
 
 _lib = None

@@ -36,8 +36,9 @@ struct FibCtx {
 };
 
 struct FibKind {
-    static constexpr int kWords = 4;  // n, join, (unused), start
-    static constexpr int kMaxOut = 2;
+    // template = the scope {n, join}; child k is fib(n-1-k)
+    static constexpr int kTmplWords = 2;
+    static constexpr int kWords = 4;
     using Ctx = FibCtx;
     struct Acc {
         unsigned long long tasks = 0, joins = 0;
@@ -49,13 +50,10 @@ struct FibKind {
             }
         }
     };
-    __device__ static uint32_t count(const uint32_t *) { return 1; }
 
-    __device__ static int roots(const Ctx &c, Acc &, uint32_t (*out)[kWords]) {
-        out[0][0] = (uint32_t)c.n;
-        out[0][1] = kFibRoot;
-        out[0][2] = 0;
-        out[0][3] = 0;
+    __device__ static int roots(const Ctx &c, Acc &, uint32_t *tmpl) {
+        tmpl[0] = (uint32_t)c.n + 1;  // child 0 of {n+1, root} is fib(n)
+        tmpl[1] = kFibRoot;
         return 1;
     }
 
@@ -72,10 +70,10 @@ struct FibKind {
         st_agent(c.result, v);
     }
 
-    __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *e, uint32_t,
-                                  uint32_t (*out)[kWords], uint32_t *err) {
+    __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
+                                  uint32_t *child, uint32_t *err) {
         acc.tasks += 1;
-        const int n = (int)e[0];
+        const int n = (int)t[0] - 1 - (int)k;
         const bool spawn = n >= 2;
         // one bump allocation per wave for every lane that opens a scope
         const unsigned long long m = __ballot(spawn);
@@ -86,7 +84,7 @@ struct FibKind {
             base = __shfl(base, leader, 64);
         }
         if (!spawn) {
-            check_out(c, acc, e[1], (unsigned long long)n);
+            check_out(c, acc, t[1], (unsigned long long)n);
             return 0;
         }
         const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
@@ -96,20 +94,14 @@ struct FibKind {
         }
         FibJoin *J = &c.joins[j];
         st_agent(&J->word, 2ull << 56);
-        st_agent(&J->parent, e[1]);
-        out[0][0] = (uint32_t)(n - 1);
-        out[0][1] = j;
-        out[0][2] = 0;
-        out[0][3] = 0;
-        out[1][0] = (uint32_t)(n - 2);
-        out[1][1] = j;
-        out[1][2] = 0;
-        out[1][3] = 0;
+        st_agent(&J->parent, t[1]);
+        child[0] = (uint32_t)n;  // children fib(n-1), fib(n-2)
+        child[1] = j;
         return 2;
     }
 };
 
-constexpr int kFibCap = 512;
+constexpr int kFibCap = 1024;  // ring items per wave (16 KiB of LDS)
 
 __global__ __launch_bounds__(64) void k_fib(FibCtx ctx, PoolView pool, SchedGlobals *g,
                                             SchedConfig cfg) {
@@ -152,15 +144,17 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     HX_HIP(hipMemsetAsync(ctx.join_next, 0, 256, m.stream));
     PoolView pool;
     HX_TRY(make_pool((uint32_t)env_int("HCLIB_HIP_DEQUES", 64),
-                     (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 16384),
-                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 8), FibKind::kWords, &pool));
-    const int grid = m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);
+                     (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
+                     (uint32_t)env_int("HCLIB_HIP_FIB_CHUNK", 8), FibKind::kWords, &pool));
+    const int grid = env_int("HCLIB_HIP_GRID", 0) > 0 ? env_int("HCLIB_HIP_GRID", 0)
+                                                    : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);
     SchedConfig cfg;
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_HI", 256);
     cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", 2);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
+    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_FIB_HUNGER", 8);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     hipLaunchKernelGGL(k_fib, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);

@@ -6,29 +6,42 @@
 //
 //   worker        = one 64-lane wave (one workgroup of 64 threads), resident
 //                   for the whole launch; a few per SIMD.
-//   local deque   = a ring of task entries in the wave's LDS (the "LDS-cached
+//   local deque   = a ring of task items in the wave's LDS (the "LDS-cached
 //                   hot end"); the owner pushes/pops at the top (LIFO,
 //                   work-first like ss_get_work, test/uts/UTS.cpp:383-402).
-//   spill/steal   = the oldest entries of a ring (the shallowest, largest
+//   spill/steal   = the oldest items of a ring (the shallowest, largest
 //                   subtrees) move as one chunk into an HBM chunk deque
-//                   (bounded MPMC ring, two per XCD); idle waves take chunks
-//                   from their own XCD's deques first, then the last deque
-//                   pushed to, then anywhere — the reference's
+//                   (bounded MPMC ring, eight per XCD); idle waves take
+//                   chunks from their own XCD's deques first, then the last
+//                   deque pushed to, then anywhere — the reference's
 //                   intra-socket-first victim order
 //                   (src/hclib-locality-graph.c:864-884) mapped to XCDs.
-//   a "task"      = one lane-item: an entry carries a count of items
-//                   (children to spawn, or 1); the wave expands up to 64 items
-//                   per batch (one per lane) by prefix sum (DPP wave scans).
+//   a "task"      = one ring item = one lane of a batch. An item is a range
+//                   [k, kend) of the children of a task template (the
+//                   parent); running it spawns child k. A task with c
+//                   children is pushed as min(c, kPieces) range items, so a
+//                   batch is simply the top min(size, 64) items. A lane
+//                   whose item still holds children k+1.. re-pushes that
+//                   residual range split in two (wide nodes such as the
+//                   2000-child T3L root fan out by doubling).
+//   ring layout   = two LDS planes: an 8-byte descriptor per item {k, kend,
+//                   delta} and the task template, stored ONCE per group of
+//                   pieces at the group's first position (delta = distance
+//                   back to it). One wave's LDS write instructions cost
+//                   ~100 cycles each whatever their lane count, so the push
+//                   is one scattered template store plus lane-contiguous
+//                   descriptor stores (one per 64 pushed items), the lane ->
+//                   group mapping coming from a tagged mark + DPP max-scan.
 //   termination   = `outstanding` = chunks in deques + waves holding work;
 //                   the launch ends when it reads 0 (the finish counter of
 //                   src/hclib-runtime.c:431-446 for the whole launch).
 //   hunger        = waves - outstanding = waves with neither work nor a
 //                   queued chunk to take; a wave gives away its oldest
-//                   entries only while that is > 0 (no chunk floods).
+//                   items only while that is > 0 (no chunk floods).
 //
 // All cross-wave words use agent-scope atomics; chunk payloads are written
-// with sc1 stores and published behind s_waitcnt + release, consumed after an
-// acquire (hx_common.h). Every spin is bounded.
+// with sc1 stores and published behind s_waitcnt, consumed with sc1 loads
+// (hx_common.h). Every spin is bounded.
 #pragma once
 
 #include "hx_common.h"
@@ -57,8 +70,18 @@ struct alignas(256) SchedGlobals {
     unsigned long long maxes[4];      // kind-specific reductions (atomic max)
 };
 
+// Diagnostic build (-DHX_STAMPS=1): per-phase s_memtime stamps, enabled at run
+// time by HCLIB_HIP_STAMPS=1. Each stamp waits for the batch's LDS traffic,
+// so the product build compiles them out of the hot loop.
+#ifndef HX_STAMPS
+#define HX_STAMPS 0
+#endif
+
 // scheduler counters (SchedGlobals::counters)
 enum : int {
+    kCtrPushCycles = 4,   // diagnostic stamps: pushing the batch's outputs
+    kCtrClockTicks = 5,   // s_memtime ticks over each wave's lifetime (clock calibration)
+    kCtrRealTicks = 6,    // s_memrealtime (100 MHz) ticks over the same span
     kCtrFormCycles = 7,   // diagnostic stamps: batch formation (scans, LDS map)
     kCtrProcCycles = 8,   // diagnostic stamps: Kind::process over the batch
     kCtrBusyCycles = 9,   // s_memtime cycles inside batches (all waves)
@@ -86,24 +109,63 @@ struct SchedConfig {
     uint32_t spin_limit; // ms a wave may stay idle before declaring a timeout
     uint32_t nwaves;     // waves in the launch (hunger = nwaves - outstanding)
     uint32_t stamps;     // diagnostic: accumulate per-phase s_memtime cycles
+    uint32_t hunger;     // batches between reads of the hunger signal (0: never give work
+                         // away unless the ring is full)
 };
 
 // Kind concept:
-//   static constexpr int kWords;      // u32 words per entry; word kWords-1 = start
-//   static constexpr int kMaxOut;     // entries one item may push
+//   static constexpr int kTmplWords;  // 2 or 6 u32 words of task template
+//   static constexpr int kWords;      // kTmplWords + 2: an item as a chunk
+//                                     // payload {template, k, kend}
 //   struct Ctx;                       // per-launch read-only parameters
 //   struct Acc { ...; __device__ void flush(SchedGlobals*); };  // per-lane stats
-//   __device__ static uint32_t count(const uint32_t *e);        // items in entry
-//   __device__ static int process(const Ctx&, Acc&, const uint32_t *e, uint32_t k,
-//                                 uint32_t (*out)[kWords], uint32_t *err);
-//   __device__ static int roots(const Ctx&, Acc&, uint32_t (*out)[kWords]);  // wave 0 only
+//   __device__ static int process(const Ctx&, Acc&, const uint32_t *tmpl, uint32_t k,
+//                                 uint32_t *child_tmpl, uint32_t *err);
+//        run child k of `tmpl`; return the number of children of the new
+//        task (0: nothing to push), whose template it wrote to child_tmpl
+//   __device__ static int roots(const Ctx&, Acc&, uint32_t *tmpl);  // wave 0 only
+
+constexpr int kPieces = 8;                // range items one task's children are pushed as
+constexpr int kGroupMax = kPieces + 2;    // items one lane pushes per batch (2 residual pieces)
+constexpr uint32_t kMaxChildren = 1u << 24;  // kend shares its descriptor word with delta
 
 template <class Kind, int CAP>
 struct WaveStack {
-    static constexpr int W = Kind::kWords;
-    uint32_t e[CAP][W];
-    int own[kWaveSize];
+    static constexpr int TW = Kind::kTmplWords;
+    static_assert(TW == 2 || TW == 6, "templates are 2 or 6 words");
+    static_assert((CAP & (CAP - 1)) == 0, "CAP must be a power of two");
+    uint2 d[CAP];                  // item descriptor {k, kend | delta << 24}
+    uint4 t0[TW == 6 ? CAP : 1];   // template words 0..3 (6-word templates)
+    uint2 t1[CAP];                 // template words 4..5 (or 0..1)
+    uint32_t mark[64];             // tagged group-start marks of the transposed push
 };
+
+template <class Kind, int CAP>
+__device__ __forceinline__ void load_tmpl(const WaveStack<Kind, CAP> &st, uint32_t slot, uint32_t *t) {
+    if constexpr (Kind::kTmplWords == 6) {
+        const uint4 a = st.t0[slot];
+        const uint2 b = st.t1[slot];
+        t[0] = a.x;
+        t[1] = a.y;
+        t[2] = a.z;
+        t[3] = a.w;
+        t[4] = b.x;
+        t[5] = b.y;
+    } else {
+        const uint2 b = st.t1[slot];
+        t[0] = b.x;
+        t[1] = b.y;
+    }
+}
+template <class Kind, int CAP>
+__device__ __forceinline__ void store_tmpl(WaveStack<Kind, CAP> &st, uint32_t slot, const uint32_t *t) {
+    if constexpr (Kind::kTmplWords == 6) {
+        st.t0[slot] = make_uint4(t[0], t[1], t[2], t[3]);
+        st.t1[slot] = make_uint2(t[4], t[5]);
+    } else {
+        st.t1[slot] = make_uint2(t[0], t[1]);
+    }
+}
 
 // ------------------------------------------------------- DPP wave scans
 // Inclusive scans over the 64 lanes with DPP row shifts and row broadcasts
@@ -189,10 +251,17 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
             __builtin_amdgcn_s_sleep(1);
         }
     }
+    // lane i packs item bot+i as {template, k, kend} (n <= 64)
     uint32_t *dst = pool.data + (size_t)slot * pool.chunk * W;
-    for (uint32_t i = lane; i < n * W; i += kWaveSize) {
-        uint32_t ent = i / W, w = i % W;
-        st_agent(&dst[i], st.e[(bot + ent) & (CAP - 1)][w]);
+    if ((uint32_t)lane < n) {
+        const uint32_t p = bot + (uint32_t)lane;
+        const uint2 dd = st.d[p & (CAP - 1)];
+        uint32_t w[W];
+        load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & (CAP - 1), w);
+        w[W - 2] = dd.x;
+        w[W - 1] = dd.y & (kMaxChildren - 1);
+#pragma unroll
+        for (int i = 0; i < W; ++i) st_agent(&dst[(uint32_t)lane * W + i], w[i]);
     }
     if (lane == 0) st_agent(&pool.cnt[slot], n);
     handoff_publish();
@@ -237,15 +306,19 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
     }
     handoff_consume();
     const uint32_t n = ld_agent(&pool.cnt[slot]);
+    // lane i unpacks item i: its own template slot (delta 0)
     const uint32_t *src = pool.data + (size_t)slot * pool.chunk * W;
-    for (uint32_t i = lane; i < n * W; i += kWaveSize) {
-        uint32_t ent = i / W, w = i % W;
-        st.e[ent][w] = ld_agent(&src[i]);
+    if ((uint32_t)lane < n) {
+        uint32_t w[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) w[i] = ld_agent(&src[(uint32_t)lane * W + i]);
+        store_tmpl<Kind, CAP>(st, (uint32_t)lane, w);
+        st.d[lane] = make_uint2(w[W - 2], w[W - 1]);
     }
     // all reads of the slot have landed before it is handed back
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) st_agent(&pool.seq[slot], pos + pool.cap);
-    __syncthreads();  // one wave per workgroup: orders the LDS ring writes
+    // one wave per workgroup: its LDS ops complete in issue order
     return n;
 }
 
@@ -256,12 +329,68 @@ __device__ __forceinline__ uint32_t xorshift(uint32_t &s) {
     return s;
 }
 
+// Push one batch's outputs at ring positions [base, base + tout). Lane L's
+// items are contiguous at base + excl: the residual of its item (children
+// k+1..kend-1 of `tmpl`, <= 2 pieces) then the new task's children (`child`,
+// ucnt children, nch = min(ucnt, kPieces) pieces). Fast path (no residuals,
+// no split): every group is children 0..nch-1 unsplit, so an item's k equals
+// its distance to the group start; the group starts are marked in LDS with a
+// per-round tag and a DPP max-scan gives every output lane its group start.
+template <class Kind, int CAP>
+__device__ __forceinline__ void push_outputs(WaveStack<Kind, CAP> &st, uint32_t base, uint32_t excl,
+                                             uint32_t tout, uint32_t nres, uint32_t ucnt,
+                                             uint32_t nch, const uint32_t *tmpl,
+                                             const uint32_t *child, uint32_t k, uint32_t kend,
+                                             uint32_t tag) {
+    constexpr uint32_t M = CAP - 1;
+    const int lane = lane_id();
+    if (__ballot(nres != 0 || ucnt > (uint32_t)kPieces) == 0) {
+        if (nch) store_tmpl<Kind, CAP>(st, (base + excl) & M, child);
+        uint32_t carry = 0;
+        for (uint32_t r0 = 0; r0 < tout; r0 += kWaveSize, ++tag) {
+            if (nch && excl >= r0 && excl < r0 + kWaveSize) st.mark[excl - r0] = tag;
+            const int s = wave_scan_max(st.mark[lane] == tag ? lane : -1);
+            const uint32_t start = s >= 0 ? r0 + (uint32_t)s : carry;
+            carry = (uint32_t)lane63((int)start);
+            const uint32_t o = r0 + (uint32_t)lane;
+            if (o < tout) {
+                const uint32_t kk = o - start;
+                st.d[(base + o) & M] = make_uint2(kk, (kk + 1) | (kk << 24));
+            }
+        }
+        return;
+    }
+    // general path: residual ranges and wide (split) child ranges
+    uint32_t pos = base + excl;
+    if (nres) {
+        store_tmpl<Kind, CAP>(st, pos & M, tmpl);  // the residual's own copy of its template
+        const uint32_t mid = k + 1 + ((kend - k - 1) >> 1);
+        st.d[pos & M] = make_uint2(k + 1, nres == 1 ? kend : mid);
+        if (nres == 2) st.d[(pos + 1) & M] = make_uint2(mid, kend | (1u << 24));
+        pos += nres;
+    }
+    if (nch) store_tmpl<Kind, CAP>(st, pos & M, child);
+    for (uint32_t j = 0; __ballot(j < nch); ++j) {
+        if (j < nch) {
+            uint32_t lo = j, hi = j + 1;
+            if (ucnt > (uint32_t)kPieces) {
+                lo = (j * ucnt) / (uint32_t)kPieces;
+                hi = ((j + 1) * ucnt) / (uint32_t)kPieces;
+            }
+            st.d[(pos + j) & M] = make_uint2(lo, hi | (j << 24));
+        }
+    }
+}
+
 template <class Kind, int CAP>
 __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, SchedGlobals *g,
                            const SchedConfig &cfg, WaveStack<Kind, CAP> &st, bool seed_roots) {
-    constexpr int W = Kind::kWords;
-    constexpr int MO = Kind::kMaxOut;
-    static_assert((CAP & (CAP - 1)) == 0, "CAP must be a power of two");
+    constexpr int TW = Kind::kTmplWords;
+    constexpr uint32_t M = CAP - 1;
+    // a push never comes within kGroupMax of the ring bottom: a spill may
+    // leave the bottom item's template up to kGroupMax-1 slots below `bot`
+    constexpr uint32_t kRoom = CAP - kGroupMax;
+    static_assert(CAP >= kWaveSize * kGroupMax + kGroupMax, "ring must hold one batch's pushes");
     const int lane = lane_id();
     const uint32_t gid = blockIdx.x;
     const uint32_t qpx = pool.nq / 8;
@@ -275,29 +404,48 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     uint32_t spins = 0;
     unsigned long long idle_since = 0;
     unsigned long long nbatch = 0, npush = 0, nsteal = 0;
-    unsigned long long cyc_busy = 0, cyc_idle = 0, cyc_spill = 0, cyc_form = 0, cyc_proc = 0;
+    unsigned long long cyc_busy = 0, cyc_idle = 0, cyc_spill = 0, cyc_form = 0, cyc_proc = 0, cyc_push = 0;
+    uint32_t tag = 1;  // mark tags: 16 per batch
+    for (int i = lane; i < kWaveSize; i += kWaveSize) st.mark[i] = 0;
 
     if (seed_roots) {
-        uint32_t out[MO > 4 ? MO : 4][W];
-        int n = Kind::roots(ctx, acc, out);
-        // roots() is uniform across the wave; lane 0's view is authoritative
-        if (lane == 0)
-            for (int i = 0; i < n; ++i)
-                for (int w = 0; w < W; ++w) st.e[i][w] = out[i][w];
-        top = n;
+        uint32_t tmpl[TW];
+        const int n = Kind::roots(ctx, acc, tmpl);  // uniform across the wave
+        uint32_t ucnt = lane == 0 && n > 0 ? (uint32_t)n : 0u;
+        if (ucnt >= kMaxChildren) {
+            dev_error(&g->err, kErrBadTask);
+            ucnt = 0;
+        }
+        const uint32_t nch = ucnt > (uint32_t)kPieces ? (uint32_t)kPieces : ucnt;
+        const uint32_t tout = lane0(nch);
+        push_outputs<Kind, CAP>(st, 0, 0, tout, 0, ucnt, nch, tmpl, tmpl, 0, 0, tag);
+        tag += 16;
+        top = tout;
         active = true;  // the host initialised outstanding = 1 for this wave
-        if (n == 0) {
+        if (top == 0) {
             active = false;
             if (lane == 0) __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
         }
-        __syncthreads();
     }
 
+    // busy/idle time is stamped only at busy<->idle transitions (a per-batch
+    // s_memtime would wait for every LDS write of the batch); the per-phase
+    // stamps of cfg.stamps are a diagnostic build that pays that wait
     unsigned long long t_mark = __builtin_amdgcn_s_memtime();
+    const unsigned long long t_begin = t_mark, rt_begin = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_batch = t_mark;  // cfg.stamps only
+    bool busy_phase = true;
     uint32_t outst_pf = 0;  // lane 0: `outstanding` as loaded one batch ago
+    uint32_t outst_cur = 0, hunger_in = 0;
     while (true) {
         const uint32_t size = top - bot;
         if (size == 0) {
+            if (busy_phase) {
+                const unsigned long long now = __builtin_amdgcn_s_memtime();
+                cyc_busy += now - t_mark;
+                t_mark = now;
+                busy_phase = false;
+            }
             if (active) {
                 active = false;
                 if (lane == 0)
@@ -324,15 +472,23 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 const unsigned long long now = __builtin_amdgcn_s_memtime();
                 cyc_idle += now - t_mark;
                 t_mark = now;
+                t_batch = now;
+                busy_phase = true;
                 continue;
             }
-            uint32_t outst = 0, e = 0;
-            if (lane == 0) {
-                outst = ld_agent(&g->outstanding);
-                e = ld_agent(&g->err);
+            // termination / error check every 8th probe: `outstanding` is one
+            // line that every idle wave would otherwise poll, and the busy
+            // waves' hunger reads queue behind those polls
+            if ((spins & 7) == 7) {
+                uint32_t outst = 0, e = 0;
+                if (lane == 0) {
+                    outst = ld_agent(&g->outstanding);
+                    e = ld_agent(&g->err);
+                }
+                if (lane0(outst) == 0 || lane0(e)) break;
+                outst_pf = outst;  // fresh hunger signal for the first batch after a steal
+                hunger_in = 0;
             }
-            if (lane0(outst) == 0 || lane0(e)) break;
-            outst_pf = outst;  // fresh hunger signal for the first batch after a steal
             // bounded idle: 100 MHz constant clock, cfg.spin_limit in ms
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
             if (spins++ == 0) idle_since = now;
@@ -349,70 +505,74 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         ++nbatch;
         // hunger signal: use the value loaded one batch ago (its latency hid
         // behind that whole batch), then issue the load for the next batch
-        const uint32_t outst = lane0(outst_pf);
-        if (lane == 0) outst_pf = ld_agent(&g->outstanding);
-        // ---- form a batch of up to 64 items from the top entries
-        uint32_t cnt = 0, start = 0, eidx = 0;
-        if ((uint32_t)lane < size) {
-            eidx = (top - 1 - lane) & (CAP - 1);
-            start = st.e[eidx][W - 1];
-            cnt = Kind::count(st.e[eidx]) - start;
+        // (loaded every cfg.hunger batches; consumed that many batches later)
+        uint32_t outst = cfg.nwaves;
+        if (cfg.hunger) {
+            if (hunger_in == 0) {
+                outst_cur = lane0(outst_pf);
+                if (lane == 0) outst_pf = ld_agent(&g->outstanding);
+                hunger_in = cfg.hunger;
+            }
+            --hunger_in;
+            outst = outst_cur;
         }
-        const int S = wave_scan_add((int)cnt);
-        const int total = lane63(S);
-        const int take = total < kWaveSize ? total : kWaveSize;
-        const int excl = S - (int)cnt;
-        st.own[lane] = -1;
-        __syncthreads();
-        if (cnt > 0 && excl < kWaveSize) st.own[excl] = lane;
-        __syncthreads();
-        // item `lane` belongs to the last entry whose first item is <= lane:
-        // two DPP max-scans give that entry and where its items start
-        const int mark = st.own[lane];
-        const int owner = wave_scan_max(mark);
-        const int owner_excl = wave_scan_max(mark >= 0 ? lane : -1);
-        const uint32_t owner_e = (top - 1 - (uint32_t)(owner < 0 ? 0 : owner)) & (CAP - 1);
-        uint32_t out[MO][W];
-        int nout = 0;
+        // ---- a batch = the top min(size, 64) items, one per lane
+        const uint32_t take = size < (uint32_t)kWaveSize ? size : (uint32_t)kWaveSize;
+        const bool has = (uint32_t)lane < take;
+        uint32_t tmpl[TW], child[TW];
+        uint32_t k = 0, kend = 0;
+        int cnt = 0;
         unsigned long long ts0 = 0;
-        if (cfg.stamps) ts0 = __builtin_amdgcn_s_memtime();
-        if (lane < take) {
-            uint32_t ent[W];
-#pragma unroll
-            for (int w = 0; w < W; ++w) ent[w] = st.e[owner_e][w];
-            const uint32_t k = ent[W - 1] + (uint32_t)(lane - owner_excl);
-            nout = Kind::process(ctx, acc, ent, k, out, &g->err);
+        if (HX_STAMPS && cfg.stamps) ts0 = __builtin_amdgcn_s_memtime();
+        if (has) {
+            const uint32_t p = top - 1 - (uint32_t)lane;
+            const uint2 dd = st.d[p & M];
+            k = dd.x;
+            kend = dd.y & (kMaxChildren - 1);
+            load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & M, tmpl);
         }
-        if (cfg.stamps) {
-            // diagnostic build only: wait for the lanes' work, then stamp
+        if (has) cnt = Kind::process(ctx, acc, tmpl, k, child, &g->err);
+        if (HX_STAMPS && cfg.stamps) {
+            // diagnostic build only
             const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
-            cyc_form += ts0 - t_mark;
+            cyc_form += ts0 - t_batch;
             cyc_proc += ts1 - ts0;
         }
-        __syncthreads();  // every lane has read its entry before the ring changes
-        // ---- retire consumed entries (0-count entries retire too)
-        const bool full = ((uint32_t)lane < size) && S <= take;
-        const uint32_t nfull = __popcll(__ballot(full));
-        // the entry just below the fully consumed ones may be partially consumed
-        if ((uint32_t)lane == nfull && (uint32_t)lane < size && excl < take)
-            st.e[eidx][W - 1] = start + (uint32_t)(take - excl);
-        top -= nfull;
-        // ---- push outputs
+        top -= take;
+        // ---- push: residual range of the item + the new task's children
+        const uint32_t rlen = has ? kend - k - 1u : 0u;
+        const uint32_t nres = rlen == 0 ? 0u : (rlen == 1 ? 1u : 2u);
+        uint32_t ucnt = cnt > 0 ? (uint32_t)cnt : 0u;
+        if (ucnt >= kMaxChildren) {
+            dev_error(&g->err, kErrBadTask);
+            ucnt = 0;
+        }
+        const uint32_t nch = ucnt > (uint32_t)kPieces ? (uint32_t)kPieces : ucnt;
+        const int nout = (int)(nres + nch);
         const int P = wave_scan_add(nout);
-        const int tout = lane63(P);
-        if ((top - bot) + (uint32_t)tout > (uint32_t)CAP) {
-            if (lane == 0) dev_error(&g->err, kErrStackOverflow);
-            break;
+        const uint32_t tout = (uint32_t)lane63(P);
+        // a push that would come near live items first moves the oldest
+        // items out as chunks (rare: only bursts of wide nodes)
+        while ((top - bot) + tout > kRoom) {
+            uint32_t n = top - bot;
+            if (n > pool.chunk) n = pool.chunk;
+            bool ok = false;
+            for (uint32_t a = 0; a < pool.nq && !ok; ++a)
+                ok = enqueue_chunk<Kind, CAP>(pool, g, (home + a) % pool.nq, st, bot, n);
+            if (!ok) {
+                if (lane == 0) dev_error(&g->err, kErrStackOverflow);
+                break;
+            }
+            ++npush;
+            bot += n;
         }
-        {
-            uint32_t p = top + (uint32_t)(P - nout);
-            for (int o = 0; o < nout; ++o, ++p)
-#pragma unroll
-                for (int w = 0; w < W; ++w) st.e[p & (CAP - 1)][w] = out[o][w];
-        }
-        top += (uint32_t)tout;
-        __syncthreads();
-        // ---- give the oldest entries to hungry waves, or relieve a full ring
+        if ((top - bot) + tout > kRoom) break;  // error already recorded
+        push_outputs<Kind, CAP>(st, top, (uint32_t)(P - nout), tout, nres, ucnt, nch, tmpl, child, k,
+                                kend, tag);
+        tag += 16;
+        top += tout;
+        if (HX_STAMPS && cfg.stamps) cyc_push += __builtin_amdgcn_s_memtime() - ts0;
+        // ---- give the oldest items to hungry waves, or relieve a full ring
         uint32_t sz = top - bot;
         uint32_t hungry = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
         if (sz > cfg.spill_hi || (hungry > 0 && sz >= cfg.spill_lo)) {
@@ -427,12 +587,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     const uint32_t q = xcc * qpx + (home - xcc * qpx + a) % qpx;
                     ok = enqueue_chunk<Kind, CAP>(pool, g, q, st, bot, n);
                 }
-                if (!ok) {
-                    if (sz > (uint32_t)(CAP - kWaveSize * MO)) {
-                        if (lane == 0) dev_error(&g->err, kErrQueueFull);
-                    }
-                    break;
-                }
+                if (!ok) break;  // deques full: keep the items (the ring still has room)
                 ++npush;
                 bot += n;
                 sz = top - bot;
@@ -440,11 +595,12 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             }
             cyc_spill += __builtin_amdgcn_s_memtime() - ts;
         }
-        const unsigned long long now = __builtin_amdgcn_s_memtime();
-        cyc_busy += now - t_mark;
-        t_mark = now;
+        if (HX_STAMPS && cfg.stamps) t_batch = __builtin_amdgcn_s_memtime();
     }
-    cyc_idle += __builtin_amdgcn_s_memtime() - t_mark;
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+    if (busy_phase) cyc_busy += t_end - t_mark;
+    else cyc_idle += t_end - t_mark;
     if (active && lane == 0) {
         // only reached on an error break: keep the protocol consistent
         __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
@@ -452,9 +608,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     acc.flush(g);
     if (lane == 0) {
         add_agent(&g->counters[kCtrBusyCycles], cyc_busy);
-        if (cfg.stamps) {
+        if (HX_STAMPS && cfg.stamps) {
             add_agent(&g->counters[kCtrFormCycles], cyc_form);
             add_agent(&g->counters[kCtrProcCycles], cyc_proc);
+            add_agent(&g->counters[kCtrPushCycles], cyc_push - cyc_proc);
         }
         add_agent(&g->counters[kCtrIdleCycles], cyc_idle);
         add_agent(&g->counters[kCtrSpillCycles], cyc_spill);
@@ -462,6 +619,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         add_agent(&g->counters[kCtrBatches], nbatch);
         add_agent(&g->counters[kCtrPushed], npush);
         add_agent(&g->counters[kCtrStolen], nsteal);
+        add_agent(&g->counters[kCtrClockTicks], t_end - t_begin);
+        add_agent(&g->counters[kCtrRealTicks], rt_end - rt_begin);
     }
 }
 

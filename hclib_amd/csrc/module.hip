@@ -44,6 +44,10 @@ __global__ void k_reset_pool(uint32_t *seq, uint32_t cap, uint32_t total) {
 }
 
 int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolView *out) {
+    if (nq < 8 || nq % 8 || cap < 2 || (cap & (cap - 1)) || chunk < 1 || chunk > 64) {
+        set_error("chunk deques: need 8k deques, power-of-two capacity, 1..64 items per chunk");
+        return HCLIB_HIP_EINVAL;
+    }
     const size_t hdr = sizeof(QueueHdr) * nq;
     const size_t slots = (size_t)nq * cap;
     const size_t need = hdr + slots * 4 * 2 + slots * chunk * words * 4 + 4096;

@@ -36,40 +36,87 @@ namespace hx {
 #define HX_W(i) \
     (w[(i) & 15] = HX_ROTL(w[((i) + 13) & 15] ^ w[((i) + 8) & 15] ^ w[((i) + 2) & 15] ^ w[(i) & 15], 1))
 
-// SHA-1 of the 16-word block w (destroyed), from the standard IV.
-__device__ __forceinline__ void sha1_block(uint32_t w[16], uint32_t h[5]) {
-    uint32_t a = 0x67452301u, b = 0xefcdab89u, c = 0x98badcfeu, d = 0x10325476u, e = 0xc3d2e1f0u;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) HX_RND(HX_F1, 0x5a827999u, w[i]);
-#pragma unroll
-    for (int i = 16; i < 20; ++i) HX_RND(HX_F1, 0x5a827999u, HX_W(i));
-#pragma unroll
-    for (int i = 20; i < 40; ++i) HX_RND(HX_F2, 0x6ed9eba1u, HX_W(i));
-#pragma unroll
-    for (int i = 40; i < 60; ++i) HX_RND(HX_F3, 0x8f1bbcdcu, HX_W(i));
-#pragma unroll
-    for (int i = 60; i < 80; ++i) HX_RND(HX_F2, 0xca62c1d6u, HX_W(i));
-    h[0] = 0x67452301u + a;
-    h[1] = 0xefcdab89u + b;
-    h[2] = 0x98badcfeu + c;
-    h[3] = 0x10325476u + d;
-    h[4] = 0xc3d2e1f0u + e;
+// rng_spawn: SHA1(parent || i) with the 24-byte message padding, specialised
+// for the one-block message W = {p0..p4, i, 0x80000000, 0 x8, 192}: the
+// schedule drops every known-zero term, the round functions are single
+// v_bitop3_b32 ops (gfx950: ch 0xCA, parity 0x96, maj 0xE8), rotates are
+// v_alignbit_b32 — ~585 VALU ops instead of ~740 for the generic block.
+// Same function as sha1_begin/hash/end of test/uts/rng/brg_sha1.c:195-327
+// applied to the rng_spawn message of brg_sha1.c:68-83.
+__device__ __forceinline__ uint32_t rl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
+__device__ __forceinline__ uint32_t fch(uint32_t b, uint32_t c, uint32_t d) {
+    return __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);
+}
+__device__ __forceinline__ uint32_t fmaj(uint32_t b, uint32_t c, uint32_t d) {
+    return __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8);
+}
+#define HX_R(F, K, W)                                       \
+    {                                                      \
+        uint32_t t_ = rl(a, 5) + F(b, c, d) + e + ((K) + (W)); \
+        e = d;                                             \
+        d = c;                                             \
+        c = rl(b, 30);                                     \
+        b = a;                                             \
+        a = t_;                                            \
+    }
 
-// rng_spawn: SHA1(parent || i) with the 24-byte message padding.
 __device__ __forceinline__ void rng_spawn_dev(const uint32_t p[5], uint32_t i, uint32_t out[5]) {
-    uint32_t w[16];
+    constexpr uint32_t C6 = 0x80000000u, C15 = 192u;  // padding word, bit length
+    constexpr uint32_t K0 = 0x5a827999u, K1 = 0x6ed9eba1u, K2 = 0x8f1bbcdcu, K3 = 0xca62c1d6u;
+    uint32_t w[80];
     w[0] = p[0];
     w[1] = p[1];
     w[2] = p[2];
     w[3] = p[3];
     w[4] = p[4];
     w[5] = i;
-    w[6] = 0x80000000u;
+    // W[t] = rotl1(W[t-3]^W[t-8]^W[t-14]^W[t-16]) with W6 = C6, W7..W14 = 0, W15 = C15
+    w[16] = rl(w[2] ^ w[0], 1);
+    w[17] = rl(w[3] ^ w[1], 1);
+    w[18] = rl(x3(C15, w[4], w[2]), 1);
+    w[19] = rl(x3(w[16], w[5], w[3]), 1);
+    w[20] = rl(x3(w[17], C6, w[4]), 1);
+    w[21] = rl(w[18] ^ w[5], 1);
+    w[22] = rl(w[19] ^ C6, 1);
+    w[23] = rl(w[20] ^ C15, 1);
 #pragma unroll
-    for (int k = 7; k < 15; ++k) w[k] = 0;
-    w[15] = 192;
-    sha1_block(w, out);
+    for (int t = 24; t < 29; ++t) w[t] = rl(w[t - 3] ^ w[t - 8], 1);
+    w[29] = rl(x3(w[26], w[21], C15), 1);
+    w[30] = rl(x3(w[27], w[22], w[16]), 1);
+    w[31] = rl(x3(w[28], w[23], w[17]) ^ C15, 1);
+#pragma unroll
+    for (int t = 32; t < 80; ++t) w[t] = rl(x3(w[t - 3], w[t - 8], w[t - 14]) ^ w[t - 16], 1);
+    uint32_t a = 0x67452301u, b = 0xefcdab89u, c = 0x98badcfeu, d = 0x10325476u, e = 0xc3d2e1f0u;
+    {  // round 0: every input but W0 is a constant (folded)
+        uint32_t t_ = rl(a, 5) + (d ^ (b & (c ^ d))) + e + K0 + w[0];
+        e = d;
+        d = c;
+        c = rl(b, 30);
+        b = a;
+        a = t_;
+    }
+#pragma unroll
+    for (int t = 1; t < 6; ++t) HX_R(fch, K0, w[t]);
+    HX_R(fch, K0, C6);
+#pragma unroll
+    for (int t = 7; t < 15; ++t) HX_R(fch, K0, 0u);
+    HX_R(fch, K0, C15);
+#pragma unroll
+    for (int t = 16; t < 20; ++t) HX_R(fch, K0, w[t]);
+#pragma unroll
+    for (int t = 20; t < 40; ++t) HX_R(x3, K1, w[t]);
+#pragma unroll
+    for (int t = 40; t < 60; ++t) HX_R(fmaj, K2, w[t]);
+#pragma unroll
+    for (int t = 60; t < 80; ++t) HX_R(x3, K3, w[t]);
+    out[0] = 0x67452301u + a;
+    out[1] = 0xefcdab89u + b;
+    out[2] = 0x98badcfeu + c;
+    out[3] = 0x10325476u + d;
+    out[4] = 0xc3d2e1f0u + e;
 }
 
 // --------------------------------------------------------- depth rules
@@ -85,13 +132,33 @@ struct UtsCtx {
     int shard, nshards, split;
     int hist_levels;
     int lds_tables;  // rules/thr fit the per-wave LDS cache
+    uint32_t bin_thr;  // BIN trees: a node has m children iff rand < bin_thr (every depth >= 1)
     int nthr;        // words in thr
     const int4 *rules;
     const uint32_t *thr;
     unsigned long long *hist;
 };
 
+constexpr size_t kUtsLdsRules = 64;     // depth rules cached in LDS per wave
+constexpr size_t kUtsLdsThr = 4 * 128;  // up to 4 GEO threshold tables
+
+// LDS copies of the rule tables (file scope, so every access is a ds_read:
+// a generic pointer to them would compile to flat loads whose waits also
+// drain the in-flight global loads).
+__shared__ int4 s_rules[kUtsLdsRules];
+__shared__ uint32_t s_thr[kUtsLdsThr];
+
+// numChildren lookup modes (the kernel is instantiated per mode)
+enum UtsMode : int {
+    kUtsRulesGlobal = 0,  // depth rules in device memory (large tables)
+    kUtsRulesLds = 1,     // depth rules cached in LDS
+    kUtsBin = 2,          // BIN tree: one rule for every depth >= 1 (no lookup at all)
+};
+
+template <int MODE>
 __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32_t *err) {
+    if (MODE == kUtsBin) return r < c.bin_thr ? c.m : 0;
+    constexpr bool LDS = MODE == kUtsRulesLds;
     int ri = d;
     if (d >= c.nrules) {
         if (!c.stationary) {
@@ -100,31 +167,36 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
         }
         ri = c.nrules - 1;
     }
-    const int4 rule = c.rules[ri];
+    const int4 rule = LDS ? s_rules[ri] : c.rules[ri];
     if (rule.x == 0) return rule.y;
     if (rule.x == 1) return r < (uint32_t)rule.y ? c.m : 0;
-    const uint32_t *t = c.thr + (size_t)rule.z * 128;
+    const int tb = rule.z * 128;
     int lo = 0, hi = 100;
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
         int mid = (lo + hi + 1) >> 1;
         if (lo < hi) {
-            if (t[mid] <= r) lo = mid;
+            const uint32_t t = LDS ? s_thr[tb + mid] : c.thr[tb + mid];
+            if (t <= r) lo = mid;
             else hi = mid - 1;
         }
     }
     return lo;
 }
 
+template <int MODE>
 struct UtsKind {
-    static constexpr int kWords = 8;  // st[5], height, nchild, start
-    static constexpr int kMaxOut = 1;
+    // template = the node {state[5], height}; an item = its children [k, kend)
+    static constexpr int kTmplWords = 6;
+    static constexpr int kWords = 8;
     using Ctx = UtsCtx;
     struct Acc {
-        unsigned long long nodes = 0, leaves = 0;
+        // per lane: at most one node per batch, so 32 bits last 4G batches
+        uint32_t nodes = 0, leaves = 0;
         uint32_t maxd = 0;
         __device__ void flush(SchedGlobals *g) {
-            unsigned long long n = wave_sum(nodes), l = wave_sum(leaves);
+            unsigned long long n = wave_sum((unsigned long long)nodes),
+                               l = wave_sum((unsigned long long)leaves);
             uint32_t m = wave_max(maxd);
             if (lane_id() == 0) {
                 add_agent(&g->counters[0], n);
@@ -133,73 +205,60 @@ struct UtsKind {
             }
         }
     };
-    __device__ static uint32_t count(const uint32_t *e) { return e[6]; }
 
-    __device__ static int roots(const Ctx &c, Acc &acc, uint32_t (*out)[kWords]) {
+    __device__ static int roots(const Ctx &c, Acc &acc, uint32_t *tmpl) {
         // the root node (height 0) is counted once, by shard 0
         if (lane_id() == 0 && c.shard == 0) {
             acc.nodes += 1;
             if (c.root_nc <= 0) acc.leaves += 1;
             if (c.hist && c.hist_levels > 0) atomicAdd(&c.hist[0], 1ull);
         }
-        if (c.root_nc <= 0) return 0;
-        for (int k = 0; k < 5; ++k) out[0][k] = c.root[k];
-        out[0][5] = 0;
-        out[0][6] = (uint32_t)c.root_nc;
-        out[0][7] = 0;
-        return 1;
+        for (int k = 0; k < 5; ++k) tmpl[k] = c.root[k];
+        tmpl[5] = 0;
+        return c.root_nc;
     }
 
-    __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *e, uint32_t k,
-                                  uint32_t (*out)[kWords], uint32_t *err) {
+    __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
+                                  uint32_t *child, uint32_t *err) {
         uint32_t ch[5];
-        rng_spawn_dev(e, k, ch);
-        for (int g = 1; g < c.gran; ++g) rng_spawn_dev(e, k, ch);  // -g: repeated spawns
-        const int h1 = (int)e[5] + 1;
+        rng_spawn_dev(t, k, ch);
+        for (int g = 1; g < c.gran; ++g) rng_spawn_dev(t, k, ch);  // -g: repeated spawns
+        const int h1 = (int)t[5] + 1;
         bool counted = true;
         if (c.nshards > 1) {
             if (h1 == c.split && (ch[0] % (uint32_t)c.nshards) != (uint32_t)c.shard) return 0;
             if (h1 < c.split && c.shard != 0) counted = false;
         }
-        const int nc = uts_nc(c, h1, ch[4] & 0x7fffffffu, err);
+        const int nc = uts_nc<MODE>(c, h1, ch[4] & 0x7fffffffu, err);
         if (counted) {
             acc.nodes += 1;
             if (nc <= 0) acc.leaves += 1;
             acc.maxd = acc.maxd > (uint32_t)h1 ? acc.maxd : (uint32_t)h1;
             if (c.hist && h1 < c.hist_levels) atomicAdd(&c.hist[h1], 1ull);
         }
-        if (nc <= 0) return 0;
-        out[0][0] = ch[0];
-        out[0][1] = ch[1];
-        out[0][2] = ch[2];
-        out[0][3] = ch[3];
-        out[0][4] = ch[4];
-        out[0][5] = (uint32_t)h1;
-        out[0][6] = (uint32_t)nc;
-        out[0][7] = 0;
-        return 1;
+        child[0] = ch[0];
+        child[1] = ch[1];
+        child[2] = ch[2];
+        child[3] = ch[3];
+        child[4] = ch[4];
+        child[5] = (uint32_t)h1;
+        return nc;
     }
 };
 
-constexpr int kUtsCap = 512;
-constexpr size_t kUtsLdsRules = 64;       // depth rules cached in LDS per wave
-constexpr size_t kUtsLdsThr = 4 * 128;    // up to 4 GEO threshold tables
+constexpr int kUtsCap = 1024;  // ring items per wave (32 KiB of LDS)
 
+template <int MODE>
 __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, SchedGlobals *g,
                                                    SchedConfig cfg) {
-    __shared__ WaveStack<UtsKind, kUtsCap> st;
-    __shared__ int4 s_rules[kUtsLdsRules];
-    __shared__ uint32_t s_thr[kUtsLdsThr];
-    UtsCtx c = ctx;
-    if (ctx.lds_tables) {
+    __shared__ WaveStack<UtsKind<MODE>, kUtsCap> st;
+    if (MODE == kUtsRulesLds) {
         // the per-node rule lookup becomes LDS-latency (no dependent HBM/L2 loads)
         for (int i = threadIdx.x; i < ctx.nrules; i += 64) s_rules[i] = ctx.rules[i];
         for (int i = threadIdx.x; i < ctx.nthr; i += 64) s_thr[i] = ctx.thr[i];
         __syncthreads();
-        c.rules = s_rules;
-        c.thr = s_thr;
     }
-    run_worker<UtsKind, kUtsCap>(c, pool, g, cfg, st, blockIdx.x == 0);
+    run_worker<UtsKind<MODE>, kUtsCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
 }
 
 // ------------------------------------------------------ host: rules/tables
@@ -453,22 +512,38 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     ctx.hist = max_levels ? d_hist : nullptr;
 
     ctx.lds_tables = (T.rules.size() <= kUtsLdsRules && T.thr.size() <= kUtsLdsThr) ? 1 : 0;
+    ctx.bin_thr = 0;
     ctx.nthr = (int)T.thr.size();
 
     PoolView pool;
     const uint32_t nq = (uint32_t)env_int("HCLIB_HIP_DEQUES", 64);
-    HX_TRY(make_pool(nq, (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 16384),
-                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 8), UtsKind::kWords, &pool));
-    const int grid = m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);
+    HX_TRY(make_pool(nq, (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
+                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 64), UtsKind<kUtsBin>::kWords, &pool));
+    // span-bound BIN trees run fastest with 2 waves per CU (fewer idle pollers,
+    // fewer hand-offs); throughput-bound GEO trees with 4
+    const bool bin = params->type == 0 && T.rules.size() == 2 && T.rules[1].x == 1 && T.stationary;
+    const int grid = env_int("HCLIB_HIP_GRID", 0) > 0
+                         ? env_int("HCLIB_HIP_GRID", 0)
+                         : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", bin ? 2 : 4);
     SchedConfig cfg;
-    cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_SPILL_HI", 320);
-    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", 24);
+    cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_SPILL_HI", 512);
+    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", 96);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
+    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", 8);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
-    hipLaunchKernelGGL(k_uts_search, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
+    if (bin) {
+        ctx.bin_thr = (uint32_t)T.rules[1].y;
+        hipLaunchKernelGGL(k_uts_search<kUtsBin>, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
+    } else if (ctx.lds_tables) {
+        hipLaunchKernelGGL(k_uts_search<kUtsRulesLds>, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals,
+                           cfg);
+    } else {
+        hipLaunchKernelGGL(k_uts_search<kUtsRulesGlobal>, dim3(grid), dim3(64), 0, m.stream, ctx, pool,
+                           m.globals, cfg);
+    }
     HX_HIP(hipGetLastError());
     HX_HIP(hipEventRecord(m.ev1, m.stream));
     SchedGlobals gl;
@@ -492,7 +567,11 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     const double busy = (double)gl.counters[kCtrBusyCycles],
                  idle = (double)gl.counters[kCtrIdleCycles];
     result->busy_frac = (busy + idle) > 0 ? busy / (busy + idle) : 0.0;
-    // s_memtime ticks at the shader clock; report with the nominal 2.4 GHz
-    result->us_per_batch = gl.counters[kCtrBatches] ? busy / gl.counters[kCtrBatches] / 2400.0 : 0.0;
+    // s_memtime ticks at the shader clock, calibrated against the 100 MHz
+    // s_memrealtime over the same wave lifetimes
+    const double mhz = gl.counters[kCtrRealTicks]
+                           ? 100.0 * (double)gl.counters[kCtrClockTicks] / (double)gl.counters[kCtrRealTicks]
+                           : 2400.0;
+    result->us_per_batch = gl.counters[kCtrBatches] ? busy / gl.counters[kCtrBatches] / mhz : 0.0;
     return HCLIB_HIP_OK;
 }

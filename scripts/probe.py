@@ -22,6 +22,12 @@ def run_uts(name, args, reps=3):
           f"Mnodes/s={best['nodes'] / best['kernel_ms'] / 1e3:.1f} batches={best['batches']} "
           f"pushed={best['chunks_pushed']} stolen={best['chunks_stolen']} busy={best['busy_frac']:.3f} "
           f"us/batch={best['us_per_batch']:.2f}", flush=True)
+    c = H.last_sched_counters()
+    if c[6]:
+        mhz = 100.0 * c[5] / c[6]
+        b = max(1, c[13])
+        print(f"   clock={mhz:.0f}MHz form_us/batch={c[7] / b / mhz:.3f} proc_us/batch={c[8] / b / mhz:.3f} "
+              f"push_us/batch={c[4] / b / mhz:.3f} spill_us/batch={c[11] / b / mhz:.3f}", flush=True)
     return best
 
 
