@@ -12,7 +12,8 @@ import os
 from typing import Optional
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "lib", "libhclib_amd.so")
+# HCLIB_AMD_LIB selects a diagnostic variant (python -m hclib_amd.build --variant X)
+LIB_PATH = os.environ.get("HCLIB_AMD_LIB") or os.path.join(PKG, "lib", "libhclib_amd.so")
 
 HCLIB_HIP_OK = 0
 FORASYNC_MODE_FLAT = 0       # inc/hclib.h:161

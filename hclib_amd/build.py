@@ -1,6 +1,10 @@
 """Build the MI355X module library in-tree with hipcc (gfx950 only).
 
     python -m hclib_amd.build        -> hclib_amd/lib/libhclib_amd.so
+    python -m hclib_amd.build --variant stamps
+                                     -> hclib_amd/lib/stamps/libhclib_amd.so (-DHX_STAMPS=1,
+                                        diagnostic per-phase cycle stamps; load it with
+                                        HCLIB_AMD_LIB=<path>; never benchmark it)
 
 The library holds every hand-written HIP kernel plus the C ABI of
 include/hclib_hip.h (modules/hip) and include/hclib.h (the HClib C API).
@@ -30,12 +34,15 @@ CFLAGS = [
 ]
 
 
-def _hash(paths):
+VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "strict": ["-DHX_STRICT_HANDOFF=1"]}
+
+
+def _hash(paths, cflags):
     h = hashlib.sha1()
     for p in paths:
         with open(p, "rb") as f:
             h.update(f.read())
-    h.update(" ".join(CFLAGS).encode())
+    h.update(" ".join(cflags).encode())
     return h.hexdigest()[:16]
 
 
@@ -46,11 +53,11 @@ def _headers():
     return hs
 
 
-def _compile(src: str, hdrs) -> str:
+def _compile(src: str, hdrs, out: str, cflags) -> str:
     path = os.path.join(CSRC, src)
-    obj = os.path.join(OUT, src.replace(".hip", "") + "." + _hash([path] + hdrs) + ".o")
+    obj = os.path.join(out, src.replace(".hip", "") + "." + _hash([path] + hdrs, cflags) + ".o")
     if not os.path.exists(obj):
-        cmd = [HIPCC] + CFLAGS + ["-c", "-x", "hip", path, "-o", obj + ".tmp"]
+        cmd = [HIPCC] + cflags + ["-c", "-x", "hip", path, "-o", obj + ".tmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
@@ -58,34 +65,38 @@ def _compile(src: str, hdrs) -> str:
     return obj
 
 
-def build(verbose: bool = True) -> str:
-    os.makedirs(OUT, exist_ok=True)
+def build(verbose: bool = True, variant: str = "") -> str:
+    out = os.path.join(OUT, variant) if variant else OUT
+    lib = os.path.join(out, "libhclib_amd.so")
+    cflags = CFLAGS + VARIANTS[variant] if variant else CFLAGS
+    os.makedirs(out, exist_ok=True)
     hdrs = _headers()
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hdrs), srcs))
-    stamp = os.path.join(OUT, ".stamp")
+        objs = list(ex.map(lambda s: _compile(s, hdrs, out, cflags), srcs))
+    stamp = os.path.join(out, ".stamp")
     key = "|".join(objs)
-    if not os.path.exists(LIB) or not os.path.exists(stamp) or open(stamp).read() != key:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs + [
+    if not os.path.exists(lib) or not os.path.exists(stamp) or open(stamp).read() != key:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + [
             "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
-        os.replace(LIB + ".tmp", LIB)
+        os.replace(lib + ".tmp", lib)
         with open(stamp, "w") as f:
             f.write(key)
     # drop stale objects
     keep = set(objs)
-    for f in os.listdir(OUT):
-        p = os.path.join(OUT, f)
+    for f in os.listdir(out):
+        p = os.path.join(out, f)
         if f.endswith(".o") and p not in keep:
             os.remove(p)
     if verbose:
-        print("built", LIB)
-    return LIB
+        print("built", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    build()
+    v = sys.argv[sys.argv.index("--variant") + 1] if "--variant" in sys.argv else ""
+    build(variant=v)
     sys.exit(0)

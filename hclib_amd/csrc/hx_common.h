@@ -52,6 +52,12 @@ __device__ __forceinline__ bool cas_agent(T *p, T expected, T desired) {
                                                 __ATOMIC_RELAXED, HX_AGENT);
 }
 
+// s_waitcnt vmcnt(0) the compiler's waitcnt pass can see (an inline-asm wait
+// is opaque to it: stores it still believes in flight make it insert a
+// vmcnt(0) before the next write to their data VGPRs — which also waits for
+// any load issued since, e.g. the one-batch-late hunger read).
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // Producer side of a hand-off: drain this wave's stores, then release.
 __device__ __forceinline__ void release_agent() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

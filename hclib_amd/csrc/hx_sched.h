@@ -204,7 +204,7 @@ __device__ __forceinline__ void handoff_publish() {
 #if HX_STRICT_HANDOFF
     release_agent();
 #else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_drain();
 #endif
 }
 __device__ __forceinline__ void handoff_consume() {
@@ -269,6 +269,8 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
         st_agent(&pool.seq[slot], pos + 1);
         st_agent(&g->hint, q);
     }
+    // nothing stays in flight past a spill (see vm_drain)
+    vm_drain();
     return true;
 }
 
@@ -316,8 +318,9 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
         st.d[lane] = make_uint2(w[W - 2], w[W - 1]);
     }
     // all reads of the slot have landed before it is handed back
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_drain();
     if (lane == 0) st_agent(&pool.seq[slot], pos + pool.cap);
+    vm_drain();
     // one wave per workgroup: its LDS ops complete in issue order
     return n;
 }
@@ -531,12 +534,18 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             kend = dd.y & (kMaxChildren - 1);
             load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & M, tmpl);
         }
+        unsigned long long tsl = 0;
+        if (HX_STAMPS && cfg.stamps) {
+            // diagnostic build only: form = loop top + pop (LDS loads landed)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            tsl = __builtin_amdgcn_s_memtime();
+            cyc_form += tsl - t_batch;
+            ts0 = tsl;
+        }
         if (has) cnt = Kind::process(ctx, acc, tmpl, k, child, &g->err);
         if (HX_STAMPS && cfg.stamps) {
-            // diagnostic build only
             const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
-            cyc_form += ts0 - t_batch;
-            cyc_proc += ts1 - ts0;
+            cyc_proc += ts1 - tsl;
         }
         top -= take;
         // ---- push: residual range of the item + the new task's children
