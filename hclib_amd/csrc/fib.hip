@@ -39,6 +39,8 @@ struct FibKind {
     // template = the scope {n, join}; child k is fib(n-1-k)
     static constexpr int kTmplWords = 2;
     static constexpr int kWords = 4;
+    static constexpr bool kPure = false;           // scopes are opened / checked out in HBM
+    static constexpr bool kBoundedChildren = true;  // 0 or 2
     using Ctx = FibCtx;
     struct Acc {
         unsigned long long tasks = 0, joins = 0;
@@ -71,7 +73,7 @@ struct FibKind {
     }
 
     __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
-                                  uint32_t *child, uint32_t *err) {
+                                  uint32_t *child, uint32_t *err, bool) {
         acc.tasks += 1;
         const int n = (int)t[0] - 1 - (int)k;
         const bool spawn = n >= 2;

@@ -124,6 +124,11 @@ struct SchedConfig {
 //        run child k of `tmpl`; return the number of children of the new
 //        task (0: nothing to push), whose template it wrote to child_tmpl
 //   __device__ static int roots(const Ctx&, Acc&, uint32_t *tmpl);  // wave 0 only
+//   static constexpr bool kPure;      // process() touches nothing but Acc: the
+//                                     // batch runs branch-free on all 64 lanes
+//                                     // (process gets `valid`; invalid lanes'
+//                                     // results are dropped)
+//   static constexpr bool kBoundedChildren;  // process() never returns >= kMaxChildren
 
 constexpr int kPieces = 8;                // range items one task's children are pushed as
 constexpr int kGroupMax = kPieces + 2;    // items one lane pushes per batch (2 residual pieces)
@@ -332,6 +337,29 @@ __device__ __forceinline__ uint32_t xorshift(uint32_t &s) {
     return s;
 }
 
+// Uniform push: no lane has a residual range and every lane that spawned a
+// task spawned exactly `mu` (<= kPieces) children — every BIN-tree batch
+// after the root fan-out, every fib batch. Group starts are then
+// mu * (rank among spawning lanes): a ballot + mbcnt, no scan, no marks.
+// Output o is child o % mu of its group, whose template sits o % mu slots
+// back (the descriptor's delta). o / mu uses a 16-bit reciprocal, exact for
+// o < 1024 and mu <= 8.
+template <class Kind, int CAP>
+__device__ __forceinline__ void push_uniform(WaveStack<Kind, CAP> &st, uint32_t base, uint32_t excl,
+                                             uint32_t tout, uint32_t mu, bool spawned,
+                                             const uint32_t *child) {
+    constexpr uint32_t M = CAP - 1;
+    if (spawned) store_tmpl<Kind, CAP>(st, (base + excl) & M, child);
+    const uint32_t rcp = (65536u + mu - 1) / mu;  // wave-uniform (scalar)
+    for (uint32_t r0 = 0; r0 < tout; r0 += kWaveSize) {
+        const uint32_t o = r0 + (uint32_t)lane_id();
+        if (o < tout) {
+            const uint32_t kk = o - ((o * rcp) >> 16) * mu;
+            st.d[(base + o) & M] = make_uint2(kk, (kk + 1) | (kk << 24));
+        }
+    }
+}
+
 // Push one batch's outputs at ring positions [base, base + tout). Lane L's
 // items are contiguous at base + excl: the residual of its item (children
 // k+1..kend-1 of `tmpl`, <= 2 pieces) then the new task's children (`child`,
@@ -488,6 +516,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     outst = ld_agent(&g->outstanding);
                     e = ld_agent(&g->err);
                 }
+                vm_drain();  // both loads land on every path (no phantom waits in the batch loop)
                 if (lane0(outst) == 0 || lane0(e)) break;
                 outst_pf = outst;  // fresh hunger signal for the first batch after a steal
                 hunger_in = 0;
@@ -527,11 +556,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         int cnt = 0;
         unsigned long long ts0 = 0;
         if (HX_STAMPS && cfg.stamps) ts0 = __builtin_amdgcn_s_memtime();
-        if (has) {
+        if (Kind::kPure || has) {  // pure kinds: every lane loads (slots wrap inside the ring)
             const uint32_t p = top - 1 - (uint32_t)lane;
             const uint2 dd = st.d[p & M];
             k = dd.x;
-            kend = dd.y & (kMaxChildren - 1);
+            kend = has ? dd.y & (kMaxChildren - 1) : k + 1;
             load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & M, tmpl);
         }
         unsigned long long tsl = 0;
@@ -542,7 +571,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             cyc_form += tsl - t_batch;
             ts0 = tsl;
         }
-        if (has) cnt = Kind::process(ctx, acc, tmpl, k, child, &g->err);
+        if constexpr (Kind::kPure) {
+            cnt = Kind::process(ctx, acc, tmpl, k, child, &g->err, has);
+        } else {
+            if (has) cnt = Kind::process(ctx, acc, tmpl, k, child, &g->err, true);
+        }
         if (HX_STAMPS && cfg.stamps) {
             const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
             cyc_proc += ts1 - tsl;
@@ -552,14 +585,27 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         const uint32_t rlen = has ? kend - k - 1u : 0u;
         const uint32_t nres = rlen == 0 ? 0u : (rlen == 1 ? 1u : 2u);
         uint32_t ucnt = cnt > 0 ? (uint32_t)cnt : 0u;
-        if (ucnt >= kMaxChildren) {
+        if (!Kind::kBoundedChildren && ucnt >= kMaxChildren) {
             dev_error(&g->err, kErrBadTask);
             ucnt = 0;
         }
         const uint32_t nch = ucnt > (uint32_t)kPieces ? (uint32_t)kPieces : ucnt;
-        const int nout = (int)(nres + nch);
-        const int P = wave_scan_add(nout);
-        const uint32_t tout = (uint32_t)lane63(P);
+        // uniform batch (see push_uniform): group size of the first spawning lane
+        const unsigned long long spawn = __ballot(nch != 0);
+        const uint32_t mu = spawn ? (uint32_t)__builtin_amdgcn_readlane((int)nch, __builtin_ctzll(spawn)) : 0u;
+        const bool uniform = __ballot(nres != 0 || ucnt > (uint32_t)kPieces || (nch != 0 && nch != mu)) == 0;
+        uint32_t tout, excl;
+        int nout = 0;
+        if (uniform) {
+            excl = mu * (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(spawn >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
+            tout = mu * (uint32_t)__builtin_popcountll(spawn);
+        } else {
+            nout = (int)(nres + nch);
+            const int P = wave_scan_add(nout);
+            tout = (uint32_t)lane63(P);
+            excl = (uint32_t)(P - nout);
+        }
         // a push that would come near live items first moves the oldest
         // items out as chunks (rare: only bursts of wide nodes)
         while ((top - bot) + tout > kRoom) {
@@ -576,9 +622,12 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             bot += n;
         }
         if ((top - bot) + tout > kRoom) break;  // error already recorded
-        push_outputs<Kind, CAP>(st, top, (uint32_t)(P - nout), tout, nres, ucnt, nch, tmpl, child, k,
-                                kend, tag);
-        tag += 16;
+        if (uniform) {
+            push_uniform<Kind, CAP>(st, top, excl, tout, mu, nch != 0, child);
+        } else {
+            push_outputs<Kind, CAP>(st, top, excl, tout, nres, ucnt, nch, tmpl, child, k, kend, tag);
+            tag += 16;
+        }
         top += tout;
         if (HX_STAMPS && cfg.stamps) cyc_push += __builtin_amdgcn_s_memtime() - ts0;
         // ---- give the oldest items to hungry waves, or relieve a full ring

@@ -184,11 +184,14 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
     return lo;
 }
 
-template <int MODE>
+// FEAT = 0: plain search; 1: sharded (nshards > 1) and/or per-level histogram
+template <int MODE, int FEAT>
 struct UtsKind {
     // template = the node {state[5], height}; an item = its children [k, kend)
     static constexpr int kTmplWords = 6;
     static constexpr int kWords = 8;
+    static constexpr bool kPure = FEAT == 0;  // the histogram's atomics are side effects
+    static constexpr bool kBoundedChildren = true;  // <= 100 (the root goes through roots())
     using Ctx = UtsCtx;
     struct Acc {
         // per lane: at most one node per batch, so 32 bits last 4G batches
@@ -219,23 +222,25 @@ struct UtsKind {
     }
 
     __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
-                                  uint32_t *child, uint32_t *err) {
+                                  uint32_t *child, uint32_t *err, bool valid) {
         uint32_t ch[5];
         rng_spawn_dev(t, k, ch);
         for (int g = 1; g < c.gran; ++g) rng_spawn_dev(t, k, ch);  // -g: repeated spawns
         const int h1 = (int)t[5] + 1;
-        bool counted = true;
-        if (c.nshards > 1) {
+        bool counted = valid;
+        if (FEAT && c.nshards > 1) {
             if (h1 == c.split && (ch[0] % (uint32_t)c.nshards) != (uint32_t)c.shard) return 0;
             if (h1 < c.split && c.shard != 0) counted = false;
         }
-        const int nc = uts_nc<MODE>(c, h1, ch[4] & 0x7fffffffu, err);
-        if (counted) {
-            acc.nodes += 1;
-            if (nc <= 0) acc.leaves += 1;
-            acc.maxd = acc.maxd > (uint32_t)h1 ? acc.maxd : (uint32_t)h1;
-            if (c.hist && h1 < c.hist_levels) atomicAdd(&c.hist[h1], 1ull);
-        }
+        // an invalid lane's template is stale ring bytes: look it up at depth 1
+        // so it can neither index past the rule table nor raise kErrDepthTable
+        int nc = uts_nc<MODE>(c, valid ? h1 : 1, ch[4] & 0x7fffffffu, err);
+        // branch-free counting (invalid lanes of a pure batch count nothing)
+        acc.nodes += counted ? 1u : 0u;
+        acc.leaves += (counted && nc <= 0) ? 1u : 0u;
+        acc.maxd = (counted && (uint32_t)h1 > acc.maxd) ? (uint32_t)h1 : acc.maxd;
+        if (FEAT && counted && c.hist && h1 < c.hist_levels) atomicAdd(&c.hist[h1], 1ull);
+        if (!valid) nc = 0;
         child[0] = ch[0];
         child[1] = ch[1];
         child[2] = ch[2];
@@ -248,17 +253,17 @@ struct UtsKind {
 
 constexpr int kUtsCap = 1024;  // ring items per wave (32 KiB of LDS)
 
-template <int MODE>
+template <int MODE, int FEAT>
 __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, SchedGlobals *g,
                                                    SchedConfig cfg) {
-    __shared__ WaveStack<UtsKind<MODE>, kUtsCap> st;
+    __shared__ WaveStack<UtsKind<MODE, FEAT>, kUtsCap> st;
     if (MODE == kUtsRulesLds) {
         // the per-node rule lookup becomes LDS-latency (no dependent HBM/L2 loads)
         for (int i = threadIdx.x; i < ctx.nrules; i += 64) s_rules[i] = ctx.rules[i];
         for (int i = threadIdx.x; i < ctx.nthr; i += 64) s_thr[i] = ctx.thr[i];
         __syncthreads();
     }
-    run_worker<UtsKind<MODE>, kUtsCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
+    run_worker<UtsKind<MODE, FEAT>, kUtsCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
 }
 
 // ------------------------------------------------------ host: rules/tables
@@ -518,7 +523,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     PoolView pool;
     const uint32_t nq = (uint32_t)env_int("HCLIB_HIP_DEQUES", 64);
     HX_TRY(make_pool(nq, (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
-                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 64), UtsKind<kUtsBin>::kWords, &pool));
+                     (uint32_t)env_int("HCLIB_HIP_CHUNK", 64), UtsKind<kUtsBin, 0>::kWords, &pool));
     // span-bound BIN trees run fastest with 2 waves per CU (fewer idle pollers,
     // fewer hand-offs); throughput-bound GEO trees with 4
     const bool bin = params->type == 0 && T.rules.size() == 2 && T.rules[1].x == 1 && T.stationary;
@@ -534,16 +539,16 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", 8);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
-    if (bin) {
-        ctx.bin_thr = (uint32_t)T.rules[1].y;
-        hipLaunchKernelGGL(k_uts_search<kUtsBin>, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
-    } else if (ctx.lds_tables) {
-        hipLaunchKernelGGL(k_uts_search<kUtsRulesLds>, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals,
-                           cfg);
-    } else {
-        hipLaunchKernelGGL(k_uts_search<kUtsRulesGlobal>, dim3(grid), dim3(64), 0, m.stream, ctx, pool,
-                           m.globals, cfg);
-    }
+    const bool feat = nshards > 1 || max_levels > 0;
+    if (bin) ctx.bin_thr = (uint32_t)T.rules[1].y;
+    const int mode = bin ? kUtsBin : (ctx.lds_tables ? kUtsRulesLds : kUtsRulesGlobal);
+    typedef void (*uts_kernel_t)(UtsCtx, PoolView, SchedGlobals *, SchedConfig);
+    static const uts_kernel_t kernels[3][2] = {
+        {k_uts_search<kUtsRulesGlobal, 0>, k_uts_search<kUtsRulesGlobal, 1>},
+        {k_uts_search<kUtsRulesLds, 0>, k_uts_search<kUtsRulesLds, 1>},
+        {k_uts_search<kUtsBin, 0>, k_uts_search<kUtsBin, 1>},
+    };
+    hipLaunchKernelGGL(kernels[mode][feat ? 1 : 0], dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
     HX_HIP(hipGetLastError());
     HX_HIP(hipEventRecord(m.ev1, m.stream));
     SchedGlobals gl;
