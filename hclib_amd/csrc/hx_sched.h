@@ -312,7 +312,9 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
         }
     }
     handoff_consume();
-    const uint32_t n = ld_agent(&pool.cnt[slot]);
+    // uniform (readfirstlane): the ring bounds derived from it stay in SGPRs,
+    // so every scheduler branch and loop of the batch is scalar
+    const uint32_t n = lane0(ld_agent(&pool.cnt[slot]));
     // lane i unpacks item i: its own template slot (delta 0)
     const uint32_t *src = pool.data + (size_t)slot * pool.chunk * W;
     if ((uint32_t)lane < n) {
@@ -469,6 +471,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     uint32_t outst_pf = 0;  // lane 0: `outstanding` as loaded one batch ago
     uint32_t outst_cur = 0, hunger_in = 0;
     while (true) {
+        // the ring bounds are wave-uniform: pin them to SGPRs (the uniformity
+        // analysis cannot see through the loop's exits) so the batch's
+        // bookkeeping is scalar and its branches are s_cbranch_scc
+        top = lane0(top);
+        bot = lane0(bot);
         const uint32_t size = top - bot;
         if (size == 0) {
             if (busy_phase) {
