@@ -94,6 +94,10 @@ typedef void (*triad_kernel_t)(float *, const float *, const float *, float, int
 
 template <int THREADS, bool CONTIG>
 static triad_kernel_t triad_pick(int v) {
+    if (v & 64) return (v & 3) == 3 ? k_triad_f32<true, true, 2, THREADS, CONTIG>
+                                    : k_triad_f32<false, true, 2, THREADS, CONTIG>;
+    if (v & 128) return (v & 3) == 3 ? k_triad_f32<true, true, 1, THREADS, CONTIG>
+                                     : k_triad_f32<false, true, 1, THREADS, CONTIG>;
     switch (v & 7) {
     case 0: return k_triad_f32<false, false, 4, THREADS, CONTIG>;
     case 1: return k_triad_f32<true, false, 4, THREADS, CONTIG>;
@@ -107,7 +111,8 @@ static triad_kernel_t triad_pick(int v) {
 }
 
 // variant bits: 1 = nt loads, 2 = nt stores, 4 = unroll 8 (else 4),
-// 8 = contiguous slice per workgroup, 16/32 = 512/1024 threads (else 256)
+// 8 = contiguous slice per workgroup, 16/32 = 512/1024 threads (else 256),
+// 64 / 128 = unroll 2 / 1 (nt stores; nt loads when bits 0-1 are 3)
 static triad_kernel_t triad_variant(int v, int *threads) {
     const bool contig = (v & 8) != 0;
     const int t = (v >> 4) & 3;
@@ -259,11 +264,12 @@ extern "C" int hclib_hip_forasync_triad_f32(float *a, const float *b, const floa
     }
     const int64_t n4 = n / 4;
     if (n4 > 0) {
-        // measured best on MI355X (scripts/probe_triad.py): one 256-thread
-        // workgroup per CU, non-temporal loads + stores, 4 pairs in flight
+        // measured best on MI355X (scripts/ubench/ub_triad.hip, scripts/probe_triad.py):
+        // one 256-thread workgroup per CU, non-temporal loads + stores, 2 (b, c)
+        // pairs per lane in flight = 16 KiB of loads per CU (32 KiB: -4 %)
         const int bpc = env_int("HCLIB_HIP_TRIAD_BLOCKS_PER_CU", 1);
         int threads = kTriadThreads;
-        triad_kernel_t k = triad_variant(env_int("HCLIB_HIP_TRIAD_VARIANT", 3), &threads);
+        triad_kernel_t k = triad_variant(env_int("HCLIB_HIP_TRIAD_VARIANT", 67), &threads);
         int64_t grid = (int64_t)mod().num_cus * bpc;
         const int64_t need = (n4 + threads - 1) / threads;
         if (grid > need) grid = need;
