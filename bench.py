@@ -53,9 +53,17 @@ def measure_triad(H, reps=20):
 
     n = 1 << 28
     g = torch.Generator(device="cuda").manual_seed(1)
-    b = torch.rand(n, device="cuda", generator=g)
-    c = torch.rand(n, device="cuda", generator=g)
-    a = torch.empty(n, device="cuda")
+    # one allocation, the three arrays staggered by 2 MiB + 4 KiB (the
+    # STREAM-style array offset: HBM channels are not all hit at the same
+    # offsets by the three streams; scripts/probe_triad_layout.py measured
+    # 0.50 ms here vs 0.50-0.54 ms for whatever separate allocations get)
+    pad = (0x201000 // 4)
+    buf = torch.empty(3 * n + 2 * pad, device="cuda")
+    b = buf[:n]
+    c = buf[n + pad:2 * n + pad]
+    a = buf[2 * n + 2 * pad:3 * n + 2 * pad]
+    b.copy_(torch.rand(n, device="cuda", generator=g))
+    c.copy_(torch.rand(n, device="cuda", generator=g))
     st = torch.cuda.current_stream()
     for _ in range(3):
         H.triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), 3.0, n, st.cuda_stream)
@@ -68,7 +76,7 @@ def measure_triad(H, reps=20):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     ok = bool(torch.equal(a, torch.add(b, torch.mul(c, 3.0))))
-    del a, b, c
+    del a, b, c, buf
     torch.cuda.empty_cache()
     algo = 12 * n  # read b, c; write a (write-allocate not counted)
     return {"ms": ms, "gbs": algo / ms / 1e6, "bytes": algo, "bit_exact": ok}
