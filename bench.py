@@ -34,6 +34,8 @@ T3L = "-t 0 -b 2000 -q 0.200014 -m 5 -r 7"
 T3L_GOLD = (111345631, 89076904, 17844)  # test/uts/sample_trees.sh:42-43
 T1 = "-t 1 -a 3 -d 10 -b 4 -r 19"
 T1_GOLD = (4130071, 3305118, 10)          # test/uts/sample_trees.sh:17-18
+T1XL = "-t 1 -a 3 -d 15 -b 4 -r 29"
+T1XL_GOLD = (1635119272, 1308100063, 15)  # test/uts/sample_trees.sh:50-51
 HBM_PEAK_GBS = 8000.0                      # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -44,6 +46,27 @@ def log(*a):
 def uts_step(H, rank, world, split):
     r = H.uts(T3L, rank, world, split) if world > 1 else H.uts(T3L)
     return r
+
+
+def wide_tree(H, rank, world, be, steps=2, split=7):
+    """The same sharded search on the wide GEO tree T1XL (1.6 G nodes,
+    throughput-bound, not span-bound): what UTS sharding does when the tree
+    has parallelism to spare. Whole-job nodes/s, max over ranks, bit-exact."""
+    from hclib_amd import dist
+
+    H.uts(T1XL, rank, world, split) if world > 1 else H.uts(T1XL)
+    dist.barrier(world, be)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = H.uts(T1XL, rank, world, split) if world > 1 else H.uts(T1XL)
+    dist.barrier(world, be)
+    el = dist.max_over_ranks(time.perf_counter() - t0, world, be)
+    tot = dist.combine_counts(r["nodes"], r["leaves"], r["max_depth"], world, be)
+    if tot != T1XL_GOLD:
+        raise SystemExit(f"T1XL mismatch: {tot} != {T1XL_GOLD}")
+    return {"workload": f"test/uts T1XL ({T1XL}) sharded over {world} GPU(s), split depth {split}",
+            "nodes_per_s": T1XL_GOLD[0] * steps / el, "ms_per_step": el * 1e3 / steps,
+            "scaling": "strong", "bit_exact": True}
 
 
 def measure_triad(H, reps=20):
@@ -124,22 +147,27 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--split", type=int, default=64, help="replicated top levels before sharding")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--backend", default="nccl",
+                    help="collective backend (nccl = RCCL; gloo only for rehearsals)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses device 0 (with --backend gloo)")
     args = ap.parse_args()
 
     import torch  # noqa: F401  (one HIP runtime for torch + the module)
 
     from hclib_amd import dist
 
-    rank, world, local = dist.init_from_env("nccl")
+    be = args.backend
+    rank, world, local = dist.init_from_env(be, share_device=args.share_device)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     import hclib_amd as H
 
-    H.init(local)
+    H.init(0 if args.share_device else local)
 
     for _ in range(args.warmup):
         r = uts_step(H, rank, world, args.split)
-    dist.barrier(world)
+    dist.barrier(world, be)
     t0 = time.perf_counter()
     kernel_ms = []
     last = None
@@ -147,12 +175,13 @@ def main():
         r = uts_step(H, rank, world, args.split)
         kernel_ms.append(r["kernel_ms"])
         last = r
-    dist.barrier(world)
-    elapsed = dist.max_over_ranks(time.perf_counter() - t0, world)
-    tot = dist.combine_counts(last["nodes"], last["leaves"], last["max_depth"], world)
+    dist.barrier(world, be)
+    elapsed = dist.max_over_ranks(time.perf_counter() - t0, world, be)
+    tot = dist.combine_counts(last["nodes"], last["leaves"], last["max_depth"], world, be)
     if tot != T3L_GOLD:
         raise SystemExit(f"T3L mismatch: {tot} != {T3L_GOLD}")
     value = T3L_GOLD[0] * args.steps / elapsed
+    wide = None if args.no_extras else wide_tree(H, rank, world, be)
     if rank != 0:
         dist.shutdown(world)
         return
@@ -178,6 +207,8 @@ def main():
             "parallelism": f"shard{world} (hash-partitioned frontier, RCCL all-reduce of counts)",
         },
     }
+    if wide:
+        out["wide_tree"] = wide
     if world == 1 and not args.no_extras:
         tri = measure_triad(H)
         traffic = load_pmc_traffic()

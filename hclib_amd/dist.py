@@ -14,25 +14,32 @@ from __future__ import annotations
 import os
 
 
-def init_from_env(backend: str = "nccl"):
+def init_from_env(backend: str = "nccl", share_device: bool = False):
     """Initialise the process group from RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*.
-    Returns (rank, world, local_rank); world == 1 needs no process group."""
+    Returns (rank, world, local_rank); world == 1 needs no process group.
+    share_device (rehearsals on a 1-GPU box, gloo only): every rank drives
+    device 0 instead of device LOCAL_RANK."""
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if share_device and backend == "nccl" and world > 1:
+        raise ValueError("share_device needs a non-RCCL backend (one GPU per RCCL rank)")
+    dev = 0 if share_device else local
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
+            if share_device:
+                torch.cuda.set_device(dev)
             dist.init_process_group(backend)
     elif backend == "nccl":
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(dev)
     return rank, world, local
 
 
@@ -71,11 +78,13 @@ def max_over_ranks(x: float, world: int, backend: str = "nccl") -> float:
 def barrier(world: int, backend: str = "nccl") -> None:
     import torch
 
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     if world > 1:
         import torch.distributed as dist
 
         dist.barrier()
-    if backend == "nccl":
+    if torch.cuda.is_available():
         torch.cuda.synchronize()
 
 
