@@ -14,6 +14,7 @@
 
 #include <vector>
 
+#include "../../include/hclib_forasync_sets.h"
 #include "hx_module.h"
 
 namespace hx {
@@ -129,12 +130,7 @@ __global__ void k_triad_tail(float *a, const float *b, const float *c, float s, 
 }
 
 // -------------------------------------------------------- generic sweep
-struct Run {
-    int first;
-    int count;
-    int stride;
-    int pad;
-};
+using hclib_sets::Run;
 
 struct DimRuns {
     const Run *runs;
@@ -204,45 +200,10 @@ __global__ __launch_bounds__(256) void k_forasync_sweep(SweepArgs A) {
 }
 
 // -------------------------------------------------- host: iteration sets
-static void add_run(std::vector<Run> &v, int lo, int hi, int stride) {
-    if (hi <= lo) return;
-    const int cnt = (int)(((int64_t)hi - lo + stride - 1) / stride);
-    if (!v.empty() && stride == 1 && v.back().stride == 1 &&
-        v.back().first + v.back().count == lo) {
-        v.back().count += cnt;  // merge contiguous unit-stride tiles
-        return;
-    }
-    v.push_back(Run{lo, cnt, stride, 0});
-}
-
-// 1-D FLAT: forasync1D_flat, src/hclib.c:316-351 (chunks counted from 0)
-static void runs_flat1d(const hclib_hip_loop_domain_t &d, std::vector<Run> &v) {
-    const int nb_chunks = d.high / d.tile;
-    const int size = d.tile * nb_chunks;
-    int low0;
-    for (low0 = d.low; low0 < size; low0 += d.tile) add_run(v, low0, low0 + d.tile, d.stride);
-    if (size < d.high) add_run(v, low0, d.high, d.stride);
-}
-
-// per-dimension FLAT tiles of the 2-D/3-D lowering (src/hclib.c:353-416)
-static void runs_flat_nd(const hclib_hip_loop_domain_t &d, std::vector<Run> &v) {
-    for (int low0 = d.low; low0 < d.high; low0 += d.tile) {
-        const int high0 = (low0 + d.tile) > d.high ? d.high : (low0 + d.tile);
-        add_run(v, low0, high0, d.stride);
-    }
-}
-
-// RECURSIVE: bisection at mid=(high+low)/2 until <= tile (src/hclib.c:158-190,
-// 192-314); leaves in index order.
-static void runs_recursive(int low, int high, const hclib_hip_loop_domain_t &d,
-                           std::vector<Run> &v) {
-    if ((high - low) > d.tile) {
-        const int mid = (high + low) / 2;
-        runs_recursive(low, mid, d, v);
-        runs_recursive(mid, high, d, v);
-    } else {
-        add_run(v, low, high, d.stride);
-    }
+// include/hclib_forasync_sets.h (shared with the C++ layers)
+static std::vector<Run> dim_runs(const hclib_hip_loop_domain_t &d, int ndim, int mode) {
+    const hclib_sets::Domain dd{d.low, d.high, d.stride, d.tile};
+    return hclib_sets::runs(dd, ndim, mode == HCLIB_HIP_FORASYNC_RECURSIVE ? 1 : 0);
 }
 
 }  // namespace hx
@@ -303,11 +264,7 @@ extern "C" int hclib_hip_forasync(int body, const void *args, int dim,
         if (domain[d].tile < 1) domain[d].tile = 1;
     }
     std::vector<Run> runs[3];
-    for (int d = 0; d < dim; ++d) {
-        if (mode == HCLIB_HIP_FORASYNC_RECURSIVE) runs_recursive(domain[d].low, domain[d].high, domain[d], runs[d]);
-        else if (dim == 1) runs_flat1d(domain[d], runs[d]);
-        else runs_flat_nd(domain[d], runs[d]);
-    }
+    for (int d = 0; d < dim; ++d) runs[d] = dim_runs(domain[d], dim, mode);
     // fast path: triad over one contiguous unit-stride run starting at 0
     if (body == HCLIB_HIP_BODY_TRIAD_F32 && runs[0].size() == 1 && runs[0][0].stride == 1 &&
         runs[0][0].first == 0) {
