@@ -49,7 +49,8 @@ def _hash(paths, cflags):
 def _headers():
     hs = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith(".h")]
     inc = os.path.join(ROOT, "include")
-    hs += [os.path.join(inc, f) for f in sorted(os.listdir(inc)) if f.endswith(".h")]
+    for d, _, fs in sorted(os.walk(inc)):
+        hs += [os.path.join(d, f) for f in sorted(fs) if f.endswith(".h")]
     return hs
 
 
@@ -96,7 +97,42 @@ def build(verbose: bool = True, variant: str = "") -> str:
     return lib
 
 
+def build_tests(verbose: bool = True) -> list:
+    """Compile the HIP C++ API test programs (tests/hip/*.hip) into
+    hclib_amd/lib/tests/ — HIP translation units of the caller's own, linked to
+    libhclib_amd.so through an $ORIGIN rpath so they run from any checkout.
+    Built here, on the CPU, never inside a GPU test."""
+    build(verbose=False)
+    tdir = os.path.join(ROOT, "tests", "hip")
+    out = os.path.join(OUT, "tests")
+    os.makedirs(out, exist_ok=True)
+    exes = []
+    for f in sorted(os.listdir(tdir)):
+        if not f.endswith(".hip"):
+            continue
+        src = os.path.join(tdir, f)
+        exe = os.path.join(out, f[:-4])
+        key = _hash([src] + _headers() + [LIB], CFLAGS)
+        stamp = exe + ".stamp"
+        if not (os.path.exists(exe) and os.path.exists(stamp) and open(stamp).read() == key):
+            cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
+                   "-I" + os.path.join(ROOT, "include"), src, "-o", exe + ".tmp", "-L" + OUT,
+                   "-lhclib_amd", "-Wl,-rpath,$ORIGIN/.."]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed for {f}:\n{r.stderr[-6000:]}")
+            os.replace(exe + ".tmp", exe)
+            with open(stamp, "w") as fh:
+                fh.write(key)
+        exes.append(exe)
+        if verbose:
+            print("built", exe)
+    return exes
+
+
 if __name__ == "__main__":
     v = sys.argv[sys.argv.index("--variant") + 1] if "--variant" in sys.argv else ""
     build(variant=v)
+    if not v:
+        build_tests()
     sys.exit(0)

@@ -7,7 +7,7 @@
 #include <string>
 
 #include "../../include/hclib_hip.h"
-#include "hx_sched.h"
+#include "../../include/hclib_hip/hx_sched.h"
 
 namespace hx {
 

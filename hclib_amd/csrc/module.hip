@@ -175,6 +175,51 @@ void hclib_hip_last_sched_counters(uint64_t out[16]) {
     for (int i = 0; i < 16; ++i) out[i] = g_mod.last_counters[i];
 }
 
+int hclib_hip_sched_begin(uint32_t entry_words, uint32_t chunk, int waves_per_cu,
+                          hclib_hip_sched_launch_t *out) {
+    if (!out || entry_words < 4 || entry_words > 64 || waves_per_cu < 1 || waves_per_cu > 8) {
+        set_error("hclib_hip_sched_begin: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    Module &m = g_mod;
+    PoolView pool;
+    HX_TRY(make_pool((uint32_t)env_int("HCLIB_HIP_DEQUES", 64), (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
+                     chunk, entry_words, &pool));
+    HX_TRY(reset_sched(pool, 1));
+    HX_HIP(hipEventRecord(m.ev0, m.stream));
+    out->hdr = pool.hdr;
+    out->seq = pool.seq;
+    out->cnt = pool.cnt;
+    out->data = pool.data;
+    out->nq = pool.nq;
+    out->cap = pool.cap;
+    out->chunk = pool.chunk;
+    out->globals = m.globals;
+    out->stream = m.stream;
+    out->grid = m.num_cus * waves_per_cu;
+    out->num_cus = m.num_cus;
+    return HCLIB_HIP_OK;
+}
+
+int hclib_hip_sched_end(const char *who, uint64_t counters[16], uint64_t maxes[4], double *kernel_ms) {
+    Module &m = g_mod;
+    if (!m.inited) {
+        set_error("hclib_hip_sched_end: no device");
+        return HCLIB_HIP_ENODEV;
+    }
+    HX_HIP(hipGetLastError());
+    HX_HIP(hipEventRecord(m.ev1, m.stream));
+    SchedGlobals gl;
+    const int rc = finish_sched(&gl, who ? who : "hclib_hip_sched_end");
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
+    if (kernel_ms) *kernel_ms = ms;
+    for (int i = 0; counters && i < 16; ++i) counters[i] = gl.counters[i];
+    for (int i = 0; maxes && i < 4; ++i) maxes[i] = gl.maxes[i];
+    return rc;
+}
+
 int hclib_hip_num_workers(void) {
     if (!g_mod.inited) return 0;
     return g_mod.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);

@@ -70,6 +70,32 @@ const char *hclib_hip_version(void);
  * [12] waves, [13] batches, [14] chunks pushed, [15] chunks stolen. */
 void hclib_hip_last_sched_counters(uint64_t out[16]);
 
+/* ----------------------------------------------- user device task kinds */
+/* The persistent-megakernel scheduler for task kinds compiled in the
+ * caller's own HIP translation unit (include/hclib_hip_cpp.h,
+ * hclib::hip::run_tasks<Kind>): begin() carves and resets the chunk deques
+ * for `entry_words` u32 per queued item, resets the scheduler globals and
+ * records the start event on the module stream; the caller launches
+ * `grid` workgroups of 64 threads on `stream`; end() records the stop
+ * event, waits, and returns the counters (see hclib_hip_last_sched_counters)
+ * and the device error, if any, as HCLIB_HIP_EDEVICE. */
+typedef struct {
+    void *hdr;         /* deque headers */
+    uint32_t *seq;     /* per-slot sequence words */
+    uint32_t *cnt;     /* per-slot item counts */
+    uint32_t *data;    /* chunk payloads */
+    uint32_t nq, cap, chunk;
+    void *globals;     /* scheduler globals (device) */
+    void *stream;      /* hipStream_t of the module */
+    int grid;          /* workgroups (waves) to launch */
+    int num_cus;
+} hclib_hip_sched_launch_t;
+
+int hclib_hip_sched_begin(uint32_t entry_words, uint32_t chunk, int waves_per_cu,
+                          hclib_hip_sched_launch_t *out);
+int hclib_hip_sched_end(const char *who, uint64_t counters[16], uint64_t maxes[4],
+                        double *kernel_ms);
+
 /* ------------------------------------------------------------ forasync */
 /* hclib_loop_domain_t of inc/hclib-task.h:53-58 (int bounds, 16 bytes). */
 typedef struct {

@@ -1,0 +1,248 @@
+/*
+ * hclib_hip_cpp.h — the device side of HClib's C++ API on MI355X
+ * (compile with hipcc --offload-arch=gfx950; link libhclib_amd.so).
+ *
+ * The reference's C++ layer runs lambdas on CPU workers
+ * (inc/hclib-async.h:161-166, inc/hclib-forasync.h:519-530). On the GPU a
+ * lambda must be device code, compiled into the caller's translation unit,
+ * so the device API is templates over the caller's functors:
+ *
+ *   hclib::hip::forasync{1,2,3}D(loop, [=] __device__ (int i[, j[, k]]) {...}, mode)
+ *       hclib::forasync{1,2,3}D with a __device__ lambda: one grid-stride
+ *       launch over exactly the reference's iteration set for `mode`
+ *       (include/hclib_forasync_sets.h). Blocking, like the reference's
+ *       finish-wrapped forasync; the _nb forms return after enqueueing.
+ *
+ *   hclib::hip::run_tasks<Kind>(ctx, &stats)
+ *       a user-defined device task kind on the persistent work-stealing
+ *       megakernel (include/hclib_hip/hx_sched.h): the GPU form of
+ *       `hclib::launch` + recursive `hclib::async` inside one `finish`. A
+ *       task is a template of Kind::kTmplWords u32 words; running child k of
+ *       a task may create one new task with n children (the Kind concept is
+ *       documented at the top of hx_sched.h). The launch-wide finish is the
+ *       scheduler's `outstanding` counter; run_tasks returns when it drains.
+ *
+ * Errors: negative HCLIB_HIP_* codes with hclib_hip_last_error(), as the
+ * module C ABI (include/hclib_hip.h).
+ */
+#ifndef HCLIB_HIP_CPP_H_
+#define HCLIB_HIP_CPP_H_
+
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "hclib_cpp.h"
+#include "hclib_hip.h"
+#include "hclib_hip/hx_sched.h"
+
+namespace hclib {
+namespace hip {
+
+// ------------------------------------------------------- device forasync
+struct RunTable {
+    const hclib_sets::Run *runs;
+    const int64_t *prefix;  // prefix[r] = iterations before run r
+    int nruns;
+};
+
+__device__ __forceinline__ int run_idx(const RunTable &t, int64_t i) {
+    int lo = 0, hi = t.nruns - 1;
+    while (lo < hi) {  // last run whose prefix <= i
+        const int mid = (lo + hi + 1) >> 1;
+        if (t.prefix[mid] <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    const hclib_sets::Run r = t.runs[lo];
+    return r.first + (int)(i - t.prefix[lo]) * r.stride;
+}
+
+// one unit-stride or strided run: no table
+template <typename F>
+__global__ __launch_bounds__(256) void k_forasync_run(hclib_sets::Run r, F f) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < r.count; t += step)
+        f(r.first + (int)t * r.stride);
+}
+
+// the cartesian product of 1-3 run tables; the innermost index varies
+// fastest so consecutive lanes touch consecutive indices
+template <int ND, typename F>
+__global__ __launch_bounds__(256) void k_forasync_runs(RunTable t0, RunTable t1, RunTable t2, int64_t n1,
+                                                       int64_t n2, int64_t total, F f) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += step) {
+        if constexpr (ND == 1) {
+            f(run_idx(t0, t));
+        } else if constexpr (ND == 2) {
+            f(run_idx(t0, t / n1), run_idx(t1, t % n1));
+        } else {
+            const int64_t r = t / n2;
+            f(run_idx(t0, r / n1), run_idx(t1, r % n1), run_idx(t2, t % n2));
+        }
+    }
+}
+
+namespace detail {
+
+inline int num_workers() {
+    const int n = hclib_hip_num_workers();
+    return n > 0 ? n : 1;
+}
+
+inline std::vector<hclib_sets::Run> dim_runs(hclib_loop_domain_t *d, int ndim, int mode) {
+    hclib_sets::resolve_tile(&d->tile, d->low, d->high, num_workers());
+    const hclib_sets::Domain dd{d->low, d->high, d->stride, d->tile};
+    return hclib_sets::runs(dd, ndim, mode);
+}
+
+inline int grid_for(int64_t total) {
+    int64_t g = (total + 255) / 256;
+    const int64_t cap = (int64_t)(hclib_hip_num_cus() > 0 ? hclib_hip_num_cus() : 256) * 8;
+    return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+// Upload the run tables of `nd` dimensions, launch, and (blocking) wait.
+template <int ND, typename F>
+int launch_runs(std::vector<hclib_sets::Run> *r, F f, hipStream_t s, bool blocking) {
+    int64_t n[3] = {1, 1, 1}, total = 1;
+    for (int d = 0; d < ND; ++d) {
+        n[d] = hclib_sets::count(r[d]);
+        total *= n[d];
+    }
+    if (total == 0) return HCLIB_HIP_OK;
+    bool single = false;
+    if constexpr (ND == 1) {
+        if (r[0].size() == 1) {
+            hipLaunchKernelGGL(k_forasync_run<F>, dim3(grid_for(total)), dim3(256), 0, s, r[0][0], f);
+            single = true;
+        }
+    }
+    if (!single) {
+        size_t bytes = 0;
+        for (int d = 0; d < ND; ++d) bytes += r[d].size() * (sizeof(hclib_sets::Run) + 8) + 8 + 64;
+        std::vector<char> h(bytes);
+        char *dbuf = nullptr;
+        if (hipMalloc((void **)&dbuf, bytes) != hipSuccess) return HCLIB_HIP_ENOMEM;
+        RunTable t[3] = {};
+        size_t off = 0;
+        for (int d = 0; d < ND; ++d) {
+            std::vector<int64_t> pre(r[d].size() + 1, 0);
+            for (size_t i = 0; i < r[d].size(); ++i) pre[i + 1] = pre[i] + r[d][i].count;
+            memcpy(&h[off], r[d].data(), r[d].size() * sizeof(hclib_sets::Run));
+            t[d].runs = (const hclib_sets::Run *)(dbuf + off);
+            off += (r[d].size() * sizeof(hclib_sets::Run) + 15) & ~(size_t)15;
+            memcpy(&h[off], pre.data(), pre.size() * 8);
+            t[d].prefix = (const int64_t *)(dbuf + off);
+            off += (pre.size() * 8 + 15) & ~(size_t)15;
+            t[d].nruns = (int)r[d].size();
+        }
+        if (hipMemcpyAsync(dbuf, h.data(), bytes, hipMemcpyHostToDevice, s) != hipSuccess) return HCLIB_HIP_EHIP;
+        hipLaunchKernelGGL((k_forasync_runs<ND, F>), dim3(grid_for(total)), dim3(256), 0, s, t[0], t[1], t[2],
+                           ND > 1 ? n[1] : 1, ND > 2 ? n[2] : 1, total, f);
+        if (blocking) {
+            if (hipStreamSynchronize(s) != hipSuccess) return HCLIB_HIP_EHIP;
+            (void)hipFree(dbuf);
+        } else {
+            (void)hipFreeAsync(dbuf, s);  // the table outlives the launch on its stream
+        }
+    }
+    if (hipGetLastError() != hipSuccess) return HCLIB_HIP_EHIP;
+    if (blocking && hipStreamSynchronize(s) != hipSuccess) return HCLIB_HIP_EHIP;
+    return HCLIB_HIP_OK;
+}
+
+template <int ND, typename F>
+int forasync(hclib_loop_domain_t *loop, F f, int mode, hipStream_t s, bool blocking) {
+    if (hclib_hip_init(0) != HCLIB_HIP_OK) return HCLIB_HIP_ENODEV;
+    std::vector<hclib_sets::Run> r[3];
+    for (int d = 0; d < ND; ++d) {
+        if (loop[d].stride < 1) return HCLIB_HIP_EINVAL;
+        r[d] = dim_runs(&loop[d], ND, mode);
+    }
+    return launch_runs<ND>(r, f, s, blocking);
+}
+
+}  // namespace detail
+
+template <typename F>
+int forasync1D(hclib::loop_domain_1d *loop, F f, int mode = FORASYNC_MODE_RECURSIVE, hipStream_t s = nullptr) {
+    return detail::forasync<1>(loop->get_internal(), f, mode, s, true);
+}
+template <typename F>
+int forasync1D_nb(hclib::loop_domain_1d *loop, F f, int mode = FORASYNC_MODE_RECURSIVE, hipStream_t s = nullptr) {
+    return detail::forasync<1>(loop->get_internal(), f, mode, s, false);
+}
+template <typename F>
+int forasync2D(hclib::loop_domain_2d *loop, F f, int mode = FORASYNC_MODE_RECURSIVE, hipStream_t s = nullptr) {
+    return detail::forasync<2>(loop->get_internal(), f, mode, s, true);
+}
+template <typename F>
+int forasync2D_nb(hclib::loop_domain_2d *loop, F f, int mode = FORASYNC_MODE_RECURSIVE, hipStream_t s = nullptr) {
+    return detail::forasync<2>(loop->get_internal(), f, mode, s, false);
+}
+template <typename F>
+int forasync3D(hclib::loop_domain_3d *loop, F f, int mode = FORASYNC_MODE_RECURSIVE, hipStream_t s = nullptr) {
+    return detail::forasync<3>(loop->get_internal(), f, mode, s, true);
+}
+template <typename F>
+int forasync3D_nb(hclib::loop_domain_3d *loop, F f, int mode = FORASYNC_MODE_RECURSIVE, hipStream_t s = nullptr) {
+    return detail::forasync<3>(loop->get_internal(), f, mode, s, false);
+}
+
+// ------------------------------------------------- user device task kinds
+template <class Kind, int CAP>
+__global__ __launch_bounds__(64) void k_run_tasks(typename Kind::Ctx ctx, hx::PoolView pool, hx::SchedGlobals *g,
+                                                  hx::SchedConfig cfg) {
+    __shared__ hx::WaveStack<Kind, CAP> st;
+    hx::run_worker<Kind, CAP>(ctx, pool, g, cfg, st, blockIdx.x == 0);
+}
+
+struct task_stats {
+    uint64_t counters[16];  // [0..7] the kind's Acc::flush counters, [8..15] scheduler
+    uint64_t maxes[4];      // the kind's atomic maxima
+    double kernel_ms;
+};
+
+struct task_config {
+    int waves_per_cu = 4;       // resident waves (workers) per CU
+    uint32_t chunk = 64;        // items per stolen chunk
+    uint32_t spill_hi = 512;    // ring occupancy that always spills
+    uint32_t spill_lo = 32;     // occupancy from which items go to hungry waves
+    uint32_t hunger = 8;        // batches between reads of the hunger signal
+    uint32_t spin_limit_ms = 20000;
+};
+
+// hclib::launch + async/finish of a device kind: wave 0 seeds Kind::roots,
+// the megakernel runs until every task (and every queued chunk) is done.
+template <class Kind, int CAP = 1024>
+int run_tasks(const typename Kind::Ctx &ctx, task_stats *stats = nullptr, const task_config &c = task_config()) {
+    hclib_hip_sched_launch_t L;
+    int rc = hclib_hip_sched_begin((uint32_t)Kind::kWords, c.chunk, c.waves_per_cu, &L);
+    if (rc != HCLIB_HIP_OK) return rc;
+    hx::PoolView pool;
+    pool.hdr = (hx::QueueHdr *)L.hdr;
+    pool.seq = L.seq;
+    pool.cnt = L.cnt;
+    pool.data = L.data;
+    pool.nq = L.nq;
+    pool.cap = L.cap;
+    pool.chunk = L.chunk;
+    hx::SchedConfig cfg;
+    cfg.spill_hi = c.spill_hi;
+    cfg.spill_lo = c.spill_lo;
+    cfg.spin_limit = c.spin_limit_ms;
+    cfg.nwaves = (uint32_t)L.grid;
+    cfg.stamps = 0;
+    cfg.hunger = c.hunger;
+    hipLaunchKernelGGL((k_run_tasks<Kind, CAP>), dim3(L.grid), dim3(64), 0, (hipStream_t)L.stream, ctx, pool,
+                       (hx::SchedGlobals *)L.globals, cfg);
+    task_stats local;
+    task_stats *s = stats ? stats : &local;
+    return hclib_hip_sched_end("hclib::hip::run_tasks", s->counters, s->maxes, &s->kernel_ms);
+}
+
+}  // namespace hip
+}  // namespace hclib
+
+#endif  // HCLIB_HIP_CPP_H_

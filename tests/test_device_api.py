@@ -1,0 +1,35 @@
+"""The device side of the C++ API (include/hclib_hip_cpp.h): a HIP program of
+the caller's own (tests/hip/device_api.hip, built by
+`python -m hclib_amd.build` / __graft_entry__.build into hclib_amd/lib/tests)
+runs forasync{1,2,3}D with __device__ lambdas against the reference's tiling
+and two user-defined task kinds (fib call tree, N-Queens) on the megakernel."""
+import os
+import subprocess
+
+import pytest
+
+import hclib_amd as H
+
+EXE = os.path.join(os.path.dirname(H.LIB_PATH), "tests", "device_api")
+
+
+def test_device_api_program_is_built():
+    assert os.path.exists(EXE), "run python -m hclib_amd.build"
+
+
+def test_device_api_fails_loudly_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    r = subprocess.run([EXE], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "hclib_hip_init" in r.stderr
+
+
+@pytest.mark.gpu
+def test_device_api_on_gpu():
+    r = subprocess.run([EXE], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Check results: OK" in r.stdout
+    assert "fib(25) = 75025" in r.stdout and "queens(12) = 14200 solutions" in r.stdout
