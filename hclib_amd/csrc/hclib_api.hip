@@ -30,6 +30,7 @@
 struct hclib_locale_t {
     int id;      // 0 = host (sysmem), 1.. = GPU index + 1
     int gpu;     // HIP device index or -1
+    int type;    // locale type (hclib_add_known_locale_type): 0 "sysmem", 1 "GPU"
 };
 
 // finish_t, src/inc/hclib-finish.h:6-10
@@ -62,8 +63,20 @@ struct Runtime {
     std::vector<hclib_task_t *> ready;  // LIFO, like the owner end of a deque
     std::map<generic_frame_ptr, int> kinds;
     std::map<void *, int> bodies;
-    hclib_locale_t host{0, -1};
-    hclib_locale_t gpu{1, 0};
+    hclib_locale_t host{0, -1, 0};
+    hclib_locale_t gpu{1, 0, 1};
+    // locale types and their memory callbacks (src/hclib-mem.c:13-50)
+    std::vector<std::string> types{"sysmem", "GPU"};
+    struct MemFuncs {
+        hclib_module_alloc_impl_func_type alloc = nullptr;
+        hclib_module_realloc_impl_func_type realloc = nullptr;
+        hclib_module_free_impl_func_type free = nullptr;
+        hclib_module_memset_impl_func_type memset = nullptr;
+        hclib_module_copy_impl_func_type copy = nullptr;
+        int copy_priority = 0;
+    };
+    std::map<int, MemFuncs> mem;
+    bool mem_builtins = false;
     // stats (HCLIB_STATS analogue, src/hclib-runtime.c:83-104)
     unsigned long long host_tasks = 0, device_tasks = 0, end_finishes = 0, forasyncs = 0;
     unsigned long long device_items = 0;
@@ -487,6 +500,251 @@ void *hclib_future_wait(hclib_future_t *f) {
 }
 
 int hclib_future_is_satisfied(hclib_future_t *f) { return f->owner->satisfied; }
+
+}  // extern "C"
+
+// ------------------------------------------- locales and memory operations
+namespace {
+
+// "sysmem" callbacks (the reference's system module registers the same
+// libc calls for its sysmem locale)
+void *host_alloc(size_t n, hclib_locale_t *) { return malloc(n ? n : 1); }
+void *host_realloc(void *p, size_t n, hclib_locale_t *) { return realloc(p, n ? n : 1); }
+void host_free(void *p, hclib_locale_t *) { free(p); }
+void host_memset(void *p, int v, size_t n, hclib_locale_t *) { memset(p, v, n); }
+void host_copy(hclib_locale_t *, void *d, hclib_locale_t *, void *s, size_t n) { memcpy(d, s, n); }
+
+// "GPU" callbacks: the MI355X counterpart of modules/cuda/src/hclib_cuda.cpp:69-139,
+// on the module's stream, each completed before its task returns
+hipStream_t gpu_stream(const char *who) {
+    ensure_gpu(who);
+    return hx::mod().stream;
+}
+void *gpu_alloc(size_t n, hclib_locale_t *) {
+    gpu_stream("hclib_allocate_at");
+    void *p = nullptr;
+    if (hipMalloc(&p, n ? n : 1) != hipSuccess) die("hclib_allocate_at: hipMalloc(%zu) failed", n);
+    return p;
+}
+void gpu_free(void *p, hclib_locale_t *) {
+    if (p && hipFree(p) != hipSuccess) die("hclib_free_at: hipFree failed");
+}
+void *gpu_realloc(void *p, size_t n, hclib_locale_t *l) {
+    void *q = gpu_alloc(n, l);
+    if (p) {
+        size_t old = 0;
+        if (hipMemPtrGetInfo(p, &old) != hipSuccess) die("hclib_reallocate_at: not a device allocation");
+        hipStream_t s = gpu_stream("hclib_reallocate_at");
+        if (hipMemcpyAsync(q, p, old < n ? old : n, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            die("hclib_reallocate_at: copy failed");
+        gpu_free(p, l);
+    }
+    return q;
+}
+void gpu_memset(void *p, int v, size_t n, hclib_locale_t *) {
+    hipStream_t s = gpu_stream("hclib_memset_at");
+    if (hipMemsetAsync(p, v, n, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        die("hclib_memset_at: hipMemsetAsync failed");
+}
+void gpu_copy(hclib_locale_t *, void *d, hclib_locale_t *, void *src, size_t n) {
+    hipStream_t s = gpu_stream("hclib_async_copy");
+    if (hipMemcpyAsync(d, src, n, hipMemcpyDefault, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        die("hclib_async_copy: hipMemcpyAsync(%zu bytes) failed", n);
+}
+
+Runtime::MemFuncs &mem_of(int type) {
+    Runtime &R = rt();
+    if (!R.mem_builtins) {
+        R.mem_builtins = true;
+        Runtime::MemFuncs &h = R.mem[0];
+        h.alloc = host_alloc;
+        h.realloc = host_realloc;
+        h.free = host_free;
+        h.memset = host_memset;
+        h.copy = host_copy;
+        h.copy_priority = MAY_USE;
+        Runtime::MemFuncs &g = R.mem[1];
+        g.alloc = gpu_alloc;
+        g.realloc = gpu_realloc;
+        g.free = gpu_free;
+        g.memset = gpu_memset;
+        g.copy = gpu_copy;
+        g.copy_priority = MUST_USE;  // modules/cuda/src/hclib_cuda.cpp:173
+    }
+    return R.mem[type];
+}
+
+hclib_locale_t *check_locale(hclib_locale_t *l, const char *who) {
+    if (!l) die("%s: NULL locale", who);
+    return l;
+}
+
+struct MemTask {  // malloc_struct / realloc_struct / memset_struct / copy_struct
+    int op;       // 0 alloc, 1 realloc, 2 memset, 3 copy
+    void *ptr;
+    size_t nbytes;
+    int pattern;
+    hclib_locale_t *locale, *src_locale;
+    void *src;
+    hclib_future_t *src_fut;
+    hclib_promise_t *promise;
+    Runtime::MemFuncs *fn;
+    hclib_module_copy_impl_func_type copy;
+};
+
+// allocate_kernel / reallocate_kernel / memset_kernel / copy_kernel,
+// src/hclib-mem.c:59-191
+void mem_task(void *raw) {
+    MemTask *m = (MemTask *)raw;
+    void *out = nullptr;
+    switch (m->op) {
+    case 0: out = m->fn->alloc(m->nbytes, m->locale); break;
+    case 1: out = m->fn->realloc(m->ptr, m->nbytes, m->locale); break;
+    case 2: m->fn->memset(m->ptr, m->pattern, m->nbytes, m->locale); break;
+    default:
+        m->copy(m->locale, m->ptr, m->src_locale, m->src ? m->src : hclib_future_get(m->src_fut), m->nbytes);
+        break;
+    }
+    hclib_promise_put(m->promise, out);
+    free(m);
+}
+
+hclib_future_t *spawn_mem(MemTask *m, hclib_future_t **futures, int nfutures) {
+    m->promise = hclib_promise_create();
+    hclib_future_t *f = hclib_get_future_for_promise(m->promise);
+    hclib_async(mem_task, m, futures, nfutures, m->locale);
+    return f;
+}
+
+MemTask *new_mem_task(int op, hclib_locale_t *l) {
+    MemTask *m = (MemTask *)calloc(1, sizeof(MemTask));
+    if (!m) die("out of memory");
+    m->op = op;
+    m->locale = l;
+    m->fn = &mem_of(l->type);
+    return m;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hclib_add_known_locale_type(const char *lbl) {  // src/hclib-locality-graph.c
+    Runtime &R = rt();
+    for (size_t i = 0; i < R.types.size(); ++i)
+        if (R.types[i] == lbl) return (int)i;
+    R.types.push_back(lbl);
+    return (int)R.types.size() - 1;
+}
+
+int hclib_get_locale_type(hclib_locale_t *l) { return check_locale(l, "hclib_get_locale_type")->type; }
+
+const char *hclib_get_locale_type_name(int type) {
+    Runtime &R = rt();
+    return (type >= 0 && type < (int)R.types.size()) ? R.types[type].c_str() : nullptr;
+}
+
+int hclib_get_num_locales(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    return 1 + (n > 0 ? 1 : 0);  // the host and the bound GPU (one GPU per process)
+}
+
+hclib_locale_t *hclib_get_locale(int index) {
+    Runtime &R = rt();
+    if (index == 0) return &R.host;
+    if (index == 1 && hclib_get_num_locales() > 1) return &R.gpu;
+    return nullptr;
+}
+
+hclib_locale_t **hclib_get_all_locales_of_type(int type, int *out_count) {
+    const int n = hclib_get_num_locales();
+    hclib_locale_t **v = (hclib_locale_t **)malloc(sizeof(hclib_locale_t *) * (size_t)(n + 1));
+    int k = 0;
+    for (int i = 0; i < n; ++i) {
+        hclib_locale_t *l = hclib_get_locale(i);
+        if (l && l->type == type) v[k++] = l;
+    }
+    if (out_count) *out_count = k;
+    return v;
+}
+
+// hclib_register_*_func, src/hclib-mem.c:23-50 (alloc/realloc/free/memset are MAY_USE)
+void hclib_register_alloc_func(int t, hclib_module_alloc_impl_func_type f) { mem_of(t).alloc = f; }
+void hclib_register_realloc_func(int t, hclib_module_realloc_impl_func_type f) { mem_of(t).realloc = f; }
+void hclib_register_free_func(int t, hclib_module_free_impl_func_type f) { mem_of(t).free = f; }
+void hclib_register_memset_func(int t, hclib_module_memset_impl_func_type f) { mem_of(t).memset = f; }
+void hclib_register_copy_func(int t, hclib_module_copy_impl_func_type f, int priority) {
+    mem_of(t).copy = f;
+    mem_of(t).copy_priority = priority;
+}
+
+hclib_future_t *hclib_allocate_at(size_t nbytes, hclib_locale_t *locale) {
+    MemTask *m = new_mem_task(0, check_locale(locale, "hclib_allocate_at"));
+    if (!m->fn->alloc) die("hclib_allocate_at: no allocator for locale type %d", locale->type);
+    m->nbytes = nbytes;
+    return spawn_mem(m, nullptr, 0);
+}
+
+hclib_future_t *hclib_reallocate_at(void *ptr, size_t new_nbytes, hclib_locale_t *locale) {
+    MemTask *m = new_mem_task(1, check_locale(locale, "hclib_reallocate_at"));
+    if (!m->fn->realloc) die("hclib_reallocate_at: no reallocator for locale type %d", locale->type);
+    m->ptr = ptr;
+    m->nbytes = new_nbytes;
+    return spawn_mem(m, nullptr, 0);
+}
+
+hclib_future_t *hclib_memset_at(void *ptr, int pattern, size_t nbytes, hclib_locale_t *locale) {
+    MemTask *m = new_mem_task(2, check_locale(locale, "hclib_memset_at"));
+    if (!m->fn->memset) die("hclib_memset_at: no memset for locale type %d", locale->type);
+    m->ptr = ptr;
+    m->pattern = pattern;
+    m->nbytes = nbytes;
+    return spawn_mem(m, nullptr, 0);
+}
+
+void hclib_free_at(void *ptr, hclib_locale_t *locale) {  // src/hclib-mem.c:148-154 (synchronous)
+    Runtime::MemFuncs &f = mem_of(check_locale(locale, "hclib_free_at")->type);
+    if (!f.free) die("hclib_free_at: no free for locale type %d", locale->type);
+    f.free(ptr, locale);
+}
+
+// src/hclib-mem.c:193-241: the MUST_USE side's copy wins; both MUST_USE is an error
+hclib_future_t *hclib_async_copy(hclib_locale_t *dst_locale, void *dst, hclib_locale_t *src_locale, void *src,
+                                 size_t nbytes, hclib_future_t **futures, const int nfutures) {
+    check_locale(dst_locale, "hclib_async_copy");
+    check_locale(src_locale, "hclib_async_copy");
+    Runtime::MemFuncs &d = mem_of(dst_locale->type), &sm = mem_of(src_locale->type);
+    hclib_module_copy_impl_func_type cb;
+    if (!d.copy && !sm.copy) die("hclib_async_copy: no copy function for locale types %d, %d", dst_locale->type,
+                                 src_locale->type);
+    if (!d.copy) cb = sm.copy;
+    else if (!sm.copy) cb = d.copy;
+    else if (d.copy == sm.copy) cb = d.copy;
+    else {
+        if (d.copy_priority == MUST_USE && sm.copy_priority == MUST_USE)
+            die("hclib_async_copy: both locales' copy functions are MUST_USE");
+        cb = sm.copy_priority == MUST_USE ? sm.copy : d.copy;
+    }
+    MemTask *m = new_mem_task(3, dst_locale);
+    m->ptr = dst;
+    m->src_locale = src_locale;
+    m->nbytes = nbytes;
+    m->copy = cb;
+    if (src == HCLIB_ASYNC_COPY_USE_FUTURE_AS_SRC) {
+        if (nfutures != 1) die("hclib_async_copy: a future source needs exactly one future");
+        m->src = nullptr;
+        m->src_fut = futures[0];
+    } else {
+        m->src = src;
+    }
+    return spawn_mem(m, futures, nfutures);
+}
+
+}  // extern "C"
+
+extern "C" {
 
 // -------------------------------------------------------------- queries
 int hclib_get_num_workers(void) {

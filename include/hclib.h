@@ -128,6 +128,45 @@ int hclib_add_module_init_function(const char *lbl, hclib_module_pre_init_func_t
                                    hclib_module_post_init_func_type post,
                                    hclib_module_finalize_func_type finalize);
 
+/* --------------------------------------- locales and memory operations */
+/* inc/hclib-locality-graph.h:123, inc/hclib-module.h:14-15, 49-97,
+ * inc/hclib.h:130-150, src/hclib-mem.c:23-241. Modules register per locale
+ * TYPE the callbacks that allocate / free / set / copy memory at a locale;
+ * the *_at calls run them as tasks at the locale and return futures. This
+ * build registers the host ("sysmem": malloc/realloc/free/memset/memcpy)
+ * and the GPU ("GPU": hipMalloc / hipFree / hipMemsetAsync /
+ * hipMemcpyAsync on the module stream; its copy callback is MUST_USE, so
+ * host<->GPU copies go through it). */
+#define MUST_USE 1
+#define MAY_USE 2
+#define HCLIB_ASYNC_COPY_USE_FUTURE_AS_SRC ((void *)0x1)
+
+typedef void *(*hclib_module_alloc_impl_func_type)(size_t, hclib_locale_t *);
+typedef void *(*hclib_module_realloc_impl_func_type)(void *, size_t, hclib_locale_t *);
+typedef void (*hclib_module_free_impl_func_type)(void *, hclib_locale_t *);
+typedef void (*hclib_module_memset_impl_func_type)(void *, int, size_t, hclib_locale_t *);
+typedef void (*hclib_module_copy_impl_func_type)(hclib_locale_t *, void *, hclib_locale_t *, void *, size_t);
+
+int hclib_add_known_locale_type(const char *lbl);
+int hclib_get_locale_type(hclib_locale_t *locale);
+const char *hclib_get_locale_type_name(int type);
+int hclib_get_num_locales(void);
+hclib_locale_t *hclib_get_locale(int index); /* 0 = host, 1.. = GPUs */
+hclib_locale_t **hclib_get_all_locales_of_type(int type, int *out_count); /* malloc'd */
+
+void hclib_register_alloc_func(int locale_type, hclib_module_alloc_impl_func_type func);
+void hclib_register_realloc_func(int locale_type, hclib_module_realloc_impl_func_type func);
+void hclib_register_free_func(int locale_type, hclib_module_free_impl_func_type func);
+void hclib_register_memset_func(int locale_type, hclib_module_memset_impl_func_type func);
+void hclib_register_copy_func(int locale_type, hclib_module_copy_impl_func_type func, int priority);
+
+hclib_future_t *hclib_allocate_at(size_t nbytes, hclib_locale_t *locale);
+hclib_future_t *hclib_reallocate_at(void *ptr, size_t new_nbytes, hclib_locale_t *locale);
+hclib_future_t *hclib_memset_at(void *ptr, int pattern, size_t nbytes, hclib_locale_t *locale);
+void hclib_free_at(void *ptr, hclib_locale_t *locale);
+hclib_future_t *hclib_async_copy(hclib_locale_t *dst_locale, void *dst, hclib_locale_t *src_locale,
+                                 void *src, size_t nbytes, hclib_future_t **futures, const int nfutures);
+
 /* --------------------------------------- modules/hip device task kinds */
 /* A host function pointer cannot run on the GPU: programs name which of
  * their functions are device task kinds / loop bodies. The argument

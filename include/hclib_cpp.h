@@ -277,6 +277,28 @@ inline auto async_future_await(T &&lambda, std::vector<hclib_future_t *> &future
                                        nullptr);
 }
 
+// ------------------------------------------------------ memory at locales
+// inc/hclib_cpp.h:58-80 (src/hclib-mem.c behind them)
+inline future_t<void *> *allocate_at(size_t nbytes, locale_t *locale) {
+    return static_cast<future_t<void *> *>(hclib_allocate_at(nbytes, locale));
+}
+inline future_t<void *> *reallocate_at(void *ptr, size_t nbytes, locale_t *locale) {
+    return static_cast<future_t<void *> *>(hclib_reallocate_at(ptr, nbytes, locale));
+}
+inline void free_at(void *ptr, locale_t *locale) { hclib_free_at(ptr, locale); }
+inline future_t<void *> *memset_at(void *ptr, int pattern, size_t nbytes, locale_t *locale) {
+    return static_cast<future_t<void *> *>(hclib_memset_at(ptr, pattern, nbytes, locale));
+}
+inline future_t<void *> *async_copy(locale_t *dst_locale, void *dst, locale_t *src_locale, void *src,
+                                    size_t nbytes) {
+    return static_cast<future_t<void *> *>(hclib_async_copy(dst_locale, dst, src_locale, src, nbytes, NULL, 0));
+}
+inline future_t<void *> *async_copy_await(locale_t *dst_locale, void *dst, locale_t *src_locale, void *src,
+                                          size_t nbytes, hclib_future_t *future) {
+    return static_cast<future_t<void *> *>(
+        hclib_async_copy(dst_locale, dst, src_locale, src, nbytes, future ? &future : NULL, future ? 1 : 0));
+}
+
 // -------------------------------------------------------------- finish
 inline void finish(std::function<void()> &&lambda) {  // inc/hclib-async.h:550-554
     hclib_start_finish();

@@ -33,13 +33,31 @@ def _run(exe, *args, timeout=300, env=None):
                           timeout=timeout, env=e)
 
 
-@pytest.mark.parametrize("name", ["promise_chain", "fib_gpu", "forasync1DCh_gpu", "uts_gpu"])
+@pytest.mark.parametrize("name", ["promise_chain", "fib_gpu", "forasync1DCh_gpu", "uts_gpu", "mem_locale"])
 def test_c_programs_compile_against_hclib_h(name):
     assert os.path.exists(_build(name))
 
 
 def test_host_promise_semantics():
     r = _run(_build("promise_chain"))
+    assert r.returncode == 0, r.stderr
+    assert "Check results: OK" in r.stdout
+
+
+def test_host_locale_memory_operations():
+    """hclib_allocate_at / reallocate_at / memset_at / async_copy / free_at at
+    the host locale (src/hclib-mem.c:23-241) and locale types."""
+    r = _run(_build("mem_locale"))
+    assert r.returncode == 0, r.stderr
+    assert "Check results: OK" in r.stdout
+
+
+@pytest.mark.gpu
+def test_gpu_locale_memory_operations():
+    """The same at the GPU locale: hipMalloc / hipMemsetAsync / hipMemcpyAsync
+    callbacks, host<->GPU round trip, realloc keeping the prefix, a copy whose
+    source is a future (HCLIB_ASYNC_COPY_USE_FUTURE_AS_SRC)."""
+    r = _run(_build("mem_locale"), "gpu")
     assert r.returncode == 0, r.stderr
     assert "Check results: OK" in r.stdout
 
