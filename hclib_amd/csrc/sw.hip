@@ -18,6 +18,7 @@
 // 64*RP-row band and sweeps the columns skewed by L (anti-diagonal
 // pipeline): at step s it computes column s-L, receiving the cell above from
 // lane L-1 through a one-lane DPP shift. Bands are chained through LDS.
+#include <stdio.h>
 #include <string.h>
 
 #include <vector>
@@ -43,6 +44,9 @@ struct SwCtx {
     uint32_t *err;
     unsigned long long *stats;  // [0] tiles, [1] releases
     uint32_t spin_ms;
+    // row-pipelined schedule: a tile's bottom row is published as 8-byte
+    // {tag = 1, H} granules — the data is the promise (R2 hand-off)
+    unsigned long long *gbot;  // [tiles][tw]
 };
 
 // alignment_score_matrix (smith_waterman.cpp:36-43) row for s2 code a, plus
@@ -63,7 +67,37 @@ __device__ __forceinline__ int shift_up1(int v) {
 // G = max3(G_left, G_up, G_diag + M + 2) — one dependent max3 per cell.
 // Inputs are converted to G when loaded, outputs back to H when stored, so
 // the promises' data (bottom row, right column, corner) are the reference's.
-__device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, int8_t *lds_s1) {
+// Diagnostic build (-DHX_STAMPS=1, `python -m hclib_amd.build --variant stamps`):
+// per-phase cycles of a tile into SwCtx::stats[4..9]; compiled out otherwise.
+#ifndef HX_STAMPS
+#define HX_STAMPS 0
+#endif
+__device__ __forceinline__ unsigned long long sw_stamp() {
+#if HX_STAMPS
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+#else
+    return 0;
+#endif
+}
+
+// ROWS = false: the three futures came through device dependency counters and
+// the inputs are global arrays (queue schedule). ROWS = true: the owning wave
+// keeps the left neighbour's right column in LDS (lds_left, H values) and the
+// top row is the up neighbour's granules, swept until every tag is set;
+// `corner` carries H at (R0-1, C0-1) in and the up tile's bottom-right out.
+template <bool ROWS>
+__device__ bool sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, int8_t *lds_s1,
+                        const int *lds_left, int *lds_right, int &corner, unsigned long long *ph) {
+    unsigned long long ts = sw_stamp();
+    auto phase = [&](int k) {
+        if (HX_STAMPS) {
+            const unsigned long long now = sw_stamp();
+            ph[k] += now - ts;
+            ts = now;
+        }
+    };
     const int lane = lane_id();
     const int i = (int)(t / (uint32_t)c.ntw) + 1;  // tile row (1-based)
     const int j = (int)(t % (uint32_t)c.ntw) + 1;  // tile col
@@ -72,18 +106,56 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
     const uint32_t tup = t - (uint32_t)c.ntw, tleft = t - 1, tdiag = t - (uint32_t)c.ntw - 1;
     // s1 segment of this tile column
     for (int q = lane; q < tw; q += 64) lds_s1[q] = c.s1[(size_t)(j - 1) * tw + q];
+    // v_perm selectors of the 4x4-blocked band: byte k of word b = s1 code - 1
+    // of column 4b+k (codes 1..4 -> 0..3, so no byte borrows)
+    uint32_t *lds_sel = (uint32_t *)(lds_s1 + ((tw + 3) & ~3));
+    if ((tw & 3) == 0)
+        for (int b = lane; b < (tw >> 2); b += 64)
+            lds_sel[b] = ((const uint32_t *)(c.s1 + (size_t)(j - 1) * tw))[b] - 0x01010101u;
     // top row = matrix row R0-1, columns C0-1 .. C0-1+tw: corner + above tile's bottom row
-    if (lane == 0) {
-        int h = (i == 1) ? -((j - 1) * tw) : (j == 1 ? -((i - 1) * th) : ld_agent(&c.corner[tdiag]));
-        if (i == 1 && j == 1) h = 0;
-        lds_top[0] = h + (R0 - 1) + (C0 - 1);
-    }
-    for (int q = lane; q < tw; q += 64) {
-        const int h = (i == 1) ? -((j - 1) * tw + q + 1) : ld_agent(&c.bottom[(size_t)tup * tw + q]);
-        lds_top[q + 1] = h + (R0 - 1) + (C0 + q);
+    if (ROWS) {
+        if (lane == 0) lds_top[0] = corner + (R0 - 1) + (C0 - 1);
+        if (i == 1) {
+            for (int q = lane; q < tw; q += 64) lds_top[q + 1] = -((j - 1) * tw + q + 1) + (R0 - 1) + (C0 + q);
+            corner = -(j * tw);  // bottom_right of boundary tile (0, j), smith_waterman.cpp:151
+        } else {
+            // sweep the up tile's granules until every tag is set (bounded)
+            const unsigned long long *g = c.gbot + (size_t)tup * tw;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            bool all = false;
+            while (!all) {
+                bool ok = true;
+                for (int q = lane; q < tw; q += 64) {
+                    const unsigned long long x = ld_agent(&g[q]);
+                    if ((x >> 32) != 1ull) ok = false;
+                    else lds_top[q + 1] = (int)(uint32_t)x + (R0 - 1) + (C0 + q);
+                }
+                all = __all(ok);
+                if (!all) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
+                        if (lane == 0) dev_error(c.err, kErrSpinTimeout);
+                        return false;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            // the next tile's diagonal corner: the up tile's bottom-right
+            corner = (int)(uint32_t)ld_agent(&g[tw - 1]);
+        }
+    } else {
+        if (lane == 0) {
+            int h = (i == 1) ? -((j - 1) * tw) : (j == 1 ? -((i - 1) * th) : ld_agent(&c.corner[tdiag]));
+            if (i == 1 && j == 1) h = 0;
+            lds_top[0] = h + (R0 - 1) + (C0 - 1);
+        }
+        for (int q = lane; q < tw; q += 64) {
+            const int h = (i == 1) ? -((j - 1) * tw + q + 1) : ld_agent(&c.bottom[(size_t)tup * tw + q]);
+            lds_top[q + 1] = h + (R0 - 1) + (C0 + q);
+        }
     }
     __syncthreads();
     for (int r0 = 0; r0 < th; r0 += 64 * kSwRP) {
+        phase(0);
         const int rfirst = r0 + lane * kSwRP;
         int left[kSwRP];
         uint32_t mrow[kSwRP];
@@ -93,7 +165,8 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
             const int r = rfirst + q;
             if (r < th) {
                 ++nvalid;
-                const int h = (j == 1) ? -((i - 1) * th + r + 1) : ld_agent(&c.right[(size_t)tleft * th + r]);
+                const int h = (j == 1) ? -((i - 1) * th + r + 1)
+                                       : (ROWS ? lds_left[r] : ld_agent(&c.right[(size_t)tleft * th + r]));
                 left[q] = h + (R0 + r) + (C0 - 1);
                 mrow[q] = sw_row2(c.s2[(size_t)(i - 1) * th + r]);
             } else {
@@ -106,7 +179,8 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
         if (rfirst == 0) up_prev = lds_top[0];
         else if (j == 1) up_prev = -((i - 1) * th + rfirst) + (R0 + rfirst - 1) + (C0 - 1);
         else up_prev = (rfirst - 1 < th)
-                           ? ld_agent(&c.right[(size_t)tleft * th + rfirst - 1]) + (R0 + rfirst - 1) + (C0 - 1)
+                           ? (ROWS ? lds_left[rfirst - 1] : ld_agent(&c.right[(size_t)tleft * th + rfirst - 1])) +
+                                 (R0 + rfirst - 1) + (C0 - 1)
                            : 0;
         const int band_rows = (th - r0) < 64 * kSwRP ? (th - r0) : 64 * kSwRP;
         const int last_lane = (band_rows - 1) / kSwRP;
@@ -118,10 +192,9 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
         int c0 = -lane < 0 ? 0 : -lane;
         int b_cur = lds_s1[c0], top_cur = lds_top[c0 + 1];
         // one anti-diagonal step of this lane's kSwRP rows
-        auto cell_rows = [&](int up) {
+        auto cell_rows_sh = [&](int up, int sh) {  // sh: bit offset of the s1 code's score byte
             int diag = up_prev;
             up_prev = up;
-            const int sh = (b_cur << 3) - 8;  // byte of the s1 code in the packed score row
 #pragma unroll
             for (int q = 0; q < kSwRP; ++q) {
                 const int d = diag + __builtin_amdgcn_sbfe((int)mrow[q], sh, 8);
@@ -133,6 +206,7 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
             }
             return up;
         };
+        auto cell_rows = [&](int up) { return cell_rows_sh(up, (b_cur << 3) - 8); };
         auto masked_step = [&](int s) {
             const int recv = shift_up1(out);
             const int cidx = s - lane;  // 0-based column
@@ -148,40 +222,140 @@ __device__ void sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
             top_cur = top_nxt;
         };
         int s = 0;
-        if (band_rows == 64 * kSwRP && tw > 64) {
+        phase(1);
+        if (band_rows == 64 * kSwRP && (tw & 3) == 0) {
+            // 4x4-blocked wavefront: at step st lane L computes its 4 rows x
+            // the 4 columns of block st-L (16 cells). The cells above come
+            // from lane L-1's previous step (4 DPP wave shifts whose `old`
+            // operand is lane 0's top row, so lane 0 needs no select); the
+            // score bytes of a row for 4 columns are one v_perm of the packed
+            // score row by the block's selector. One DPP latency per 16
+            // cells, no LDS round trip in the dependency chain.
+            const int nblocks = tw >> 2, nsteps = nblocks + 63;
+            int o0 = 0, o1 = 0, o2 = 0, o3 = 0;  // row-3 outputs of this lane's last block
+            // the block's selector and top values are loaded one step ahead
+            // (their LDS latency hides behind a step's arithmetic)
+            auto clampb = [&](int b) { return b < 0 ? 0 : (b >= nblocks ? nblocks - 1 : b); };
+            int cbn = clampb(-lane);
+            uint32_t sel_n = lds_sel[cbn];
+            int t0n = lds_top[4 * cbn + 1], t1n = lds_top[4 * cbn + 2], t2n = lds_top[4 * cbn + 3],
+                t3n = lds_top[4 * cbn + 4];
+            for (int st = 0; st < nsteps; ++st) {
+                const int blk = st - lane;
+                const bool valid = blk >= 0 && blk < nblocks;
+                const uint32_t sel = sel_n;
+                const int u0 = __builtin_amdgcn_update_dpp(t0n, o0, 0x138, 0xf, 0xf, false);
+                const int u1 = __builtin_amdgcn_update_dpp(t1n, o1, 0x138, 0xf, 0xf, false);
+                const int u2 = __builtin_amdgcn_update_dpp(t2n, o2, 0x138, 0xf, 0xf, false);
+                const int u3 = __builtin_amdgcn_update_dpp(t3n, o3, 0x138, 0xf, 0xf, false);
+                cbn = clampb(blk + 1);
+                sel_n = lds_sel[cbn];
+                t0n = lds_top[4 * cbn + 1];
+                t1n = lds_top[4 * cbn + 2];
+                t2n = lds_top[4 * cbn + 3];
+                t3n = lds_top[4 * cbn + 4];
+                if (valid) {
+                    uint32_t pm[kSwRP];
+#pragma unroll
+                    for (int q = 0; q < kSwRP; ++q) pm[q] = __builtin_amdgcn_perm(0u, mrow[q], sel);
+                    const int uu[4] = {u0, u1, u2, u3};
+                    int ov[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        int diag = jj == 0 ? up_prev : uu[jj - 1];
+                        int up = uu[jj];
+#pragma unroll
+                        for (int q = 0; q < kSwRP; ++q) {
+                            const int d = diag + (int)(int8_t)(pm[q] >> (8 * jj));
+                            const int a = left[q] > up ? left[q] : up;
+                            const int h = a > d ? a : d;
+                            diag = left[q];
+                            left[q] = h;
+                            up = h;
+                        }
+                        ov[jj] = up;
+                    }
+                    up_prev = u3;
+                    o0 = ov[0];
+                    o1 = ov[1];
+                    o2 = ov[2];
+                    o3 = ov[3];
+                    if (lane == 63) {  // the band's last row
+                        int *bp = &lds_bot[4 * blk + 1];
+                        bp[0] = o0;
+                        bp[1] = o1;
+                        bp[2] = o2;
+                        bp[3] = o3;
+                    }
+                }
+            }
+            s = steps;
+        } else if (band_rows == 64 * kSwRP && tw > 64) {
             // ramp-in, a branch-free steady state in which every lane is on a
             // valid column (s-63 .. s), then ramp-out
             for (; s < 63; ++s) masked_step(s);
-            const int dummy = tw + 2 + lane;  // lds_bot has 64 spare words past tw+1
-            for (; s < tw; ++s) {
-                const int recv = shift_up1(out);
-                const int cidx = s - lane;
-                const int cn = cidx + 1 < tw ? cidx + 1 : tw - 1;
-                const int b_nxt = lds_s1[cn];
-                const int top_nxt = lds_top[cn + 1];
-                out = cell_rows(lane == 0 ? top_cur : recv);
-                // lane 63 owns the band's last row; the others hit a private dummy word
-                lds_bot[(lane == 63) ? cidx + 1 : dummy] = out;
-                b_cur = b_nxt;
-                top_cur = top_nxt;
+            phase(2);
+            // Register pipeline, no LDS round trip per step: lane L's s1 code
+            // for column s-L is lane L-1's from step s-1 (one DPP shift), as
+            // is the cell above; lane 0 takes the new column's code and top
+            // value from a 64-column chunk (readlane + lane-0 select), and lane
+            // 63's bottom-row outputs collect in a chunk stored once per 64
+            // steps. LDS is touched three times per 64 columns.
+            int shv = lane <= 62 ? (((int)lds_s1[62 - lane]) << 3) - 8 : 0;  // column 62-L
+            for (int s0 = 63; s0 < tw; s0 += 64) {
+                const int nblk = (tw - s0) < 64 ? (tw - s0) : 64;
+                const int cc = s0 + lane;
+                const int csh = cc < tw ? (((int)lds_s1[cc]) << 3) - 8 : 0;
+                const int ctop = cc < tw ? lds_top[cc + 1] : 0;
+                int botc = 0;
+                for (int k = 0; k < nblk; ++k) {
+                    const int up_in = shift_up1(out), sh_in = shift_up1(shv);
+                    const int top_k = __builtin_amdgcn_readlane(ctop, k), sh_k = __builtin_amdgcn_readlane(csh, k);
+                    const int recv = lane == 0 ? top_k : up_in;
+                    shv = lane == 0 ? sh_k : sh_in;
+                    out = cell_rows_sh(recv, shv);
+                    const int b63 = __builtin_amdgcn_readlane(out, 63);
+                    botc = lane == k ? b63 : botc;
+                }
+                // lane 63 computed columns s0-63 .. s0-63+nblk-1 (the band's last row)
+                if (lane < nblk) lds_bot[s0 - 63 + lane + 1] = botc;
+                s = s0 + nblk;
             }
+            // masked_step's operands for step s (column s-L)
+            const int cn = (s - lane) < tw ? (s - lane) : tw - 1;
+            b_cur = lds_s1[cn];
+            top_cur = lds_top[cn + 1];
         }
+        phase(3);
         for (; s < steps; ++s) masked_step(s);
-        // the right column H[row][tw] is each lane's final `left`
+        phase(4);
+        // the right column H[row][tw] is each lane's final `left`; in the
+        // row schedule it stays in LDS for the same wave's next tile
 #pragma unroll
         for (int q = 0; q < kSwRP; ++q)
-            if (q < nvalid)
-                st_agent(&c.right[(size_t)t * th + rfirst + q],
-                         left[q] - (R0 + rfirst + q) - (C0 + tw - 1));
+            if (q < nvalid) {
+                const int hv = left[q] - (R0 + rfirst + q) - (C0 + tw - 1);
+                if (ROWS) lds_right[rfirst + q] = hv;
+                else st_agent(&c.right[(size_t)t * th + rfirst + q], hv);
+            }
         __syncthreads();
         // the band's bottom row becomes the next band's top row (both in G)
         for (int q = lane; q <= tw; q += 64) lds_top[q] = lds_bot[q];
         __syncthreads();
     }
     const int Rb = R0 + th - 1;  // matrix row of the tile's bottom row
-    for (int q = lane; q < tw; q += 64)
-        st_agent(&c.bottom[(size_t)t * tw + q], lds_top[q + 1] - Rb - (C0 + q));
-    if (lane == 0) st_agent(&c.corner[t], lds_top[tw] - Rb - (C0 + tw - 1));
+    if (ROWS) {
+        // publish: one 8-byte sc1 granule per value (tag 1 = put), drained
+        for (int q = lane; q < tw; q += 64)
+            st_agent(&c.gbot[(size_t)t * tw + q],
+                     (1ull << 32) | (unsigned long long)(uint32_t)(lds_top[q + 1] - Rb - (C0 + q)));
+    } else {
+        for (int q = lane; q < tw; q += 64)
+            st_agent(&c.bottom[(size_t)t * tw + q], lds_top[q + 1] - Rb - (C0 + q));
+        if (lane == 0) st_agent(&c.corner[t], lds_top[tw] - Rb - (C0 + tw - 1));
+    }
+    phase(5);
+    return true;
 }
 
 __global__ __launch_bounds__(64) void k_sw(SwCtx c) {
@@ -192,6 +366,7 @@ __global__ __launch_bounds__(64) void k_sw(SwCtx c) {
     const int lane = lane_id();
     const uint32_t ntiles = (uint32_t)(c.ntw * c.nth);
     unsigned long long ntile = 0, nrel = 0, cyc_tile = 0, cyc_rel = 0;
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
     while (true) {
         uint32_t ticket = 0;
         if (lane == 0) ticket = add_agent(c.ready_head, 1u);
@@ -215,7 +390,8 @@ __global__ __launch_bounds__(64) void k_sw(SwCtx c) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        sw_tile(c, t, lds_top, lds_bot, lds_s1);
+        int corner_unused = 0;
+        sw_tile<false>(c, t, lds_top, lds_bot, lds_s1, nullptr, nullptr, corner_unused, ph);
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         cyc_tile += t1 - t0;
         ++ntile;
@@ -246,6 +422,49 @@ __global__ __launch_bounds__(64) void k_sw(SwCtx c) {
         add_agent(&c.stats[1], nrel);
         add_agent(&c.stats[2], cyc_tile);
         add_agent(&c.stats[3], cyc_rel);
+        if (HX_STAMPS)
+            for (int k = 0; k < 6; ++k) add_agent(&c.stats[4 + k], ph[k]);
+    }
+}
+
+// Row schedule ("owner computes"): wave w owns tile rows w, w + W, ... and
+// runs each left to right. Tile (i, j)'s three futures: the left one is the
+// wave's own previous tile (program order; its right column stays in LDS),
+// the up one is the up tile's published granules (swept, R2 hand-off), the
+// diagonal one is implied (the up row's owner finished (i-1, j-1) before
+// (i-1, j)). Every wave is resident (grid <= CUs) and rows complete in
+// order, so each wait ends.
+__global__ __launch_bounds__(64) void k_sw_rows(SwCtx c) {
+    extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+    int *lds_top = sw_lds;
+    int *lds_bot = sw_lds + ((c.tw + 1 + 3) & ~3);
+    int *lds_left = lds_bot + ((c.tw + 1 + 3) & ~3) + 68;  // + 64 dummy words
+    int *lds_right = lds_left + ((c.th + 3) & ~3);             // swapped per tile
+    int8_t *lds_s1 = (int8_t *)(lds_right + ((c.th + 3) & ~3));
+    const int lane = lane_id();
+    unsigned long long ntile = 0, cyc_tile = 0, cyc_wait = 0;
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+    bool ok = true;
+    for (int i = blockIdx.x; i < c.nth && ok; i += gridDim.x) {
+        int corner = (i == 0) ? 0 : -(i * c.th);  // H(R0-1, C0-1) of tile (i, 0): boundary column
+        for (int j = 0; j < c.ntw && ok; ++j) {
+            const uint32_t t = (uint32_t)(i * c.ntw + j);
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+            ok = sw_tile<true>(c, t, lds_top, lds_bot, lds_s1, lds_left, lds_right, corner, ph);
+            vm_drain();  // every granule of this tile is out before the next one is computed
+            int *tmp = lds_left;  // this tile's right column is the next tile's left
+            lds_left = lds_right;
+            lds_right = tmp;
+            cyc_tile += __builtin_amdgcn_s_memtime() - t0;
+            ++ntile;
+        }
+    }
+    if (lane == 0) {
+        add_agent(&c.stats[0], ntile);
+        add_agent(&c.stats[2], cyc_tile);
+        add_agent(&c.stats[3], cyc_wait);
+        if (HX_STAMPS)
+            for (int k = 0; k < 6; ++k) add_agent(&c.stats[4 + k], ph[k]);
     }
 }
 
@@ -279,13 +498,20 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         if (s2[k] < 1 || s2[k] > 4) { set_error("hclib_hip_sw: s2 must be coded 1..4"); return HCLIB_HIP_EINVAL; }
     HX_TRY(ensure_device());
     Module &m = mod();
+    // schedule: "rows" (default) = owner-computes tile rows with granule
+    // hand-offs; "queue" = the generic DAG: dependency counters + ready list
+    const char *sched = getenv("HCLIB_HIP_SW_SCHED");
+    // the row schedule keeps two tile columns in LDS: wide tiles fall back
+    const size_t rows_lds = 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + 68 * 4 + 2 * (size_t)((tw + 3) & ~3) + 16 +
+                            2 * (size_t)(((th + 3) & ~3) * 4);
+    const bool rows = !(sched && !strcmp(sched, "queue")) && rows_lds <= 64 * 1024;
     const size_t nt = ntw * nth;
     const size_t b_s1 = ntw * tw, b_s2 = nth * th;
-    const size_t b_bot = nt * tw * 4, b_right = nt * th * 4, b_c = nt * 4, b_dep = nt * 4,
-                 b_ready = nt * 4;
+    const size_t b_bot = rows ? 0 : nt * tw * 4, b_right = rows ? 0 : nt * th * 4, b_c = nt * 4,
+                 b_dep = nt * 4, b_ready = nt * 4, b_gbot = rows ? nt * tw * 8 : 0;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t total = al(b_s1) + al(b_s2) + al(b_bot) + al(b_right) + al(b_c) + al(b_dep) +
-                         al(b_ready) + 1024;
+                         al(b_ready) + al(b_gbot) + 1024;
     char *d = nullptr;
     if (hipMalloc((void **)&d, total) != hipSuccess) {
         set_error("hclib_hip_sw: hipMalloc(%zu) failed", total);
@@ -300,6 +526,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     c.corner = (int *)(d + off); off += al(b_c);
     c.deps = (uint32_t *)(d + off); off += al(b_dep);
     c.ready = (uint32_t *)(d + off); off += al(b_ready);
+    c.gbot = (unsigned long long *)(d + off); off += al(b_gbot);
     uint32_t *misc = (uint32_t *)(d + off);
     c.ready_tail = misc;
     c.ready_head = misc + 64;
@@ -319,27 +546,49 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         uint32_t one = 1;  // tile 0 already sits at ready[0]
         if ((rc = hip_check(hipMemcpyAsync(c.ready_tail, &one, 4, hipMemcpyHostToDevice, m.stream), "tail"))) return fail(rc);
     }
-    hipLaunchKernelGGL(k_sw_init, dim3(1024), dim3(256), 0, m.stream, c.deps, c.ready, c.ntw, c.nth);
-    const size_t lds = 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + 68 * 4 + (size_t)tw + 16;
-    if (lds > 160 * 1024) return fail((set_error("hclib_hip_sw: tile width too large for LDS"), HCLIB_HIP_EINVAL));
+    if (rows) {
+        // every granule's tag starts at 0 (not yet put)
+        if ((rc = hip_check(hipMemsetAsync(c.gbot, 0, b_gbot, m.stream), "memset granules"))) return fail(rc);
+    } else {
+        hipLaunchKernelGGL(k_sw_init, dim3(1024), dim3(256), 0, m.stream, c.deps, c.ready, c.ntw, c.nth);
+    }
+    const size_t lds = 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + 68 * 4 + 2 * (size_t)((tw + 3) & ~3) + 16 +
+                       (rows ? 2 * (size_t)(((th + 3) & ~3) * 4) : 0);
+    if (lds > 160 * 1024) return fail((set_error("hclib_hip_sw: tile too large for LDS"), HCLIB_HIP_EINVAL));
     int per_cu = (int)((160 * 1024) / lds);
-    int wpc = env_int("HCLIB_HIP_SW_WAVES_PER_CU", 2);
+    // rows: one wave per CU owns tile rows (all resident, so every wait ends)
+    int wpc = env_int("HCLIB_HIP_SW_WAVES_PER_CU", rows ? 1 : 2);
     if (wpc > per_cu) wpc = per_cu;
     if (wpc < 1) wpc = 1;
-    const int grid = m.num_cus * wpc;
-    if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute((const void *)k_sw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    int grid = m.num_cus * wpc;
+    if (rows && grid > (int)nth) grid = (int)nth;
+    const void *kern = rows ? (const void *)k_sw_rows : (const void *)k_sw;
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if ((rc = hip_check(hipEventRecord(m.ev0, m.stream), "event"))) return fail(rc);
-    hipLaunchKernelGGL(k_sw, dim3(grid), dim3(64), lds, m.stream, c);
+    if (rows) hipLaunchKernelGGL(k_sw_rows, dim3(grid), dim3(64), lds, m.stream, c);
+    else hipLaunchKernelGGL(k_sw, dim3(grid), dim3(64), lds, m.stream, c);
     if ((rc = hip_check(hipGetLastError(), "k_sw launch"))) return fail(rc);
     if ((rc = hip_check(hipEventRecord(m.ev1, m.stream), "event"))) return fail(rc);
     uint32_t herr = 0;
-    unsigned long long st[4] = {0, 0, 0, 0};
+    unsigned long long st[10] = {0};
     int corner = 0;
     if ((rc = hip_check(hipStreamSynchronize(m.stream), "k_sw"))) return fail(rc);
     (void)hipMemcpy(&herr, c.err, 4, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(st, c.stats, 32, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(&corner, c.corner + (nt - 1), 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(st, c.stats, sizeof(st), hipMemcpyDeviceToHost);
+    if (HX_STAMPS && st[0])
+        fprintf(stderr, "sw phases (cycles/tile): inputs %.0f band-setup %.0f ramp-in %.0f steady %.0f ramp-out %.0f outputs %.0f\n",
+                (double)st[4] / st[0], (double)st[5] / st[0], (double)st[6] / st[0], (double)st[7] / st[0],
+                (double)st[8] / st[0], (double)st[9] / st[0]);
+    if (rows) {
+        unsigned long long g = 0;  // bottom_row[tw-1] of the last tile (its granule)
+        (void)hipMemcpy(&g, c.gbot + (nt * tw - 1), 8, hipMemcpyDeviceToHost);
+        corner = (int)(uint32_t)g;
+        // the edges the row schedule resolved: each tile's up, left and
+        // diagonal futures (the same 3-per-interior-tile count as the queue)
+        st[1] = 3ull * (ntw - 1) * (nth - 1) + (ntw - 1) + (nth - 1);
+    } else {
+        (void)hipMemcpy(&corner, c.corner + (nt - 1), 4, hipMemcpyDeviceToHost);
+    }
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
     (void)hipFree(d);
