@@ -105,6 +105,27 @@ def measure_triad(H, reps=20):
     return {"ms": ms, "gbs": algo / ms / 1e6, "bytes": algo, "bit_exact": ok}
 
 
+def measure_atomics(H, fib_stats):
+    """L2 atomic throughput of the fib megakernel (BASELINE north_star: the
+    fraction of peak L2 atomic throughput). Algorithmic atomics: one
+    returning 64-bit fetch-add per task check-out (tasks - 1; the root's
+    result is a store), the reference's check_out_finish
+    (src/hclib-runtime.c:431-446). Peak: the same access shape saturated by
+    hclib_hip_atomic_calibrate (every lane, random 16-B records), measured
+    here in the same process; the hot-word and coalesced shapes are
+    reported beside it."""
+    scatter, _ = H.atomic_calibrate(H.ATOMIC_SCATTER_RET64, 256)
+    hot, _ = H.atomic_calibrate(H.ATOMIC_HOT_WORD, 256)
+    coal, _ = H.atomic_calibrate(H.ATOMIC_COALESCED32, 256)
+    ops = fib_stats["tasks"] - 1
+    achieved = ops / (fib_stats["kernel_ms"] * 1e-3) / 1e6
+    return {"kernel": "k_fib (fib(30) join check-outs)", "unit": "Mops/s",
+            "algorithmic_atomics_per_launch": ops, "achieved": achieved,
+            "peak": scatter, "frac": achieved / scatter,
+            "peak_shape": "returning 64-bit add, every lane its own random 16-B record (256 MiB)",
+            "hot_word_peak": hot, "coalesced32_peak": coal}
+
+
 def load_pmc_traffic():
     """HBM bytes per triad launch from the committed rocprofv3 PMC summary
     (profiles/), corrected per MI355X_MICROARCH.md (FETCH_SIZE x2 on gfx950)."""
@@ -247,6 +268,7 @@ def main():
             "sw_64k": {"cells_per_s": swst["cells_per_s"], "kernel_ms": swst["kernel_ms"],
                        "score": score},
         }
+        out["atomics"] = measure_atomics(H, fst)
         threads = int(os.environ.get("HCLIB_BENCH_CPU_THREADS",
                                      os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))))
         threads = max(1, min(threads, 16, os.cpu_count() or 1))

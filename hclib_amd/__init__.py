@@ -109,6 +109,8 @@ def lib():
         L.hclib_hip_fib.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(FibResult)]
         L.hclib_hip_sw.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_int,
                                    C.c_int, C.POINTER(C.c_int), C.POINTER(SwResult)]
+        L.hclib_hip_atomic_calibrate.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double),
+                                                 C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -218,6 +220,19 @@ def sw_map(text: bytes) -> bytes:
     """clear_whitespaces_do_mapping (smith_waterman.cpp:45-59): keep ACGT -> 1..4."""
     table = bytes.maketrans(b"ACGT", b"\x01\x02\x03\x04")
     return bytes(x for x in text if x in b"ACGT").translate(table)
+
+
+ATOMIC_SCATTER_RET64 = 0  # include/hclib_hip.h
+ATOMIC_HOT_WORD = 1
+ATOMIC_COALESCED32 = 2
+
+
+def atomic_calibrate(mode: int, iters: int = 256):
+    """Saturated L2 atomic rate of one access shape: (Mops/s, kernel ms)."""
+    r, ms = C.c_double(), C.c_double()
+    _check(lib().hclib_hip_atomic_calibrate(mode, iters, C.byref(r), C.byref(ms)),
+           "hclib_hip_atomic_calibrate")
+    return r.value, ms.value
 
 
 def last_sched_counters():

@@ -70,6 +70,21 @@ const char *hclib_hip_version(void);
  * [12] waves, [13] batches, [14] chunks pushed, [15] chunks stolen. */
 void hclib_hip_last_sched_counters(uint64_t out[16]);
 
+/* L2 atomic-throughput calibration: the saturated rate (million atomic
+ * ops per second, whole GPU) of one access shape the runtime's atomics use,
+ * the "peak" fib/SW/scheduler atomic rates are priced against.
+ *   0 HCLIB_HIP_ATOMIC_SCATTER_RET64: every lane a returning 64-bit add on
+ *     its own random 16-B record (fib join check-out, SW dependency counters)
+ *   1 HCLIB_HIP_ATOMIC_HOT_WORD: lane 0 of every wave on ONE shared word
+ *     (deque tickets, the `outstanding` termination counter)
+ *   2 HCLIB_HIP_ATOMIC_COALESCED32: 64 consecutive non-returning 32-bit adds
+ *     per wave instruction (the L2 atomic units' streaming peak)
+ * `iters` atomic ops per lane (mode 1: per wave). */
+#define HCLIB_HIP_ATOMIC_SCATTER_RET64 0
+#define HCLIB_HIP_ATOMIC_HOT_WORD 1
+#define HCLIB_HIP_ATOMIC_COALESCED32 2
+int hclib_hip_atomic_calibrate(int mode, int iters, double *mops_per_s, double *kernel_ms);
+
 /* ----------------------------------------------- user device task kinds */
 /* The persistent-megakernel scheduler for task kinds compiled in the
  * caller's own HIP translation unit (include/hclib_hip_cpp.h,

@@ -99,3 +99,13 @@ def test_compute_entry_points_fail_loudly_without_gpu():
         H.fib(10)
     with pytest.raises(H.HclibError):
         H.uts("-t 1 -a 3 -d 10 -b 4 -r 19")
+    with pytest.raises(H.HclibError):
+        H.atomic_calibrate(H.ATOMIC_SCATTER_RET64, 16)
+
+
+def test_atomic_calibrate_rejects_bad_arguments():
+    """Argument checks run before any device call (no GPU needed)."""
+    with pytest.raises(H.HclibError):
+        H.atomic_calibrate(3, 16)
+    with pytest.raises(H.HclibError):
+        H.atomic_calibrate(H.ATOMIC_HOT_WORD, 1)

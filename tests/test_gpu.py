@@ -259,3 +259,13 @@ def test_sw_both_schedules(golden, sched, monkeypatch):
         b = bytes(rng.integers(1, 5, n2, dtype=np.int8).tobytes())
         score, _ = H.sw(a, b, tw, th)
         assert score == L.sw_score(a, b, tw, th), (n1, n2, tw, th)
+
+
+def test_atomic_calibration_shapes():
+    """The three L2 atomic shapes run and rank as the hardware must: a single
+    hot word is far slower than atomics spread over many lines, and the
+    coalesced streaming shape is the fastest."""
+    scatter, _ = H.atomic_calibrate(H.ATOMIC_SCATTER_RET64, 64)
+    hot, _ = H.atomic_calibrate(H.ATOMIC_HOT_WORD, 64)
+    coal, _ = H.atomic_calibrate(H.ATOMIC_COALESCED32, 64)
+    assert 0 < hot < scatter < coal
