@@ -19,19 +19,16 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <ucontext.h>
 
 #include <map>
 #include <string>
 #include <vector>
 
 #include "../../include/hclib.h"
+#include "../../include/hclib_forasync_sets.h"
 #include "hx_module.h"
 
-struct hclib_locale_t {
-    int id;      // 0 = host (sysmem), 1.. = GPU index + 1
-    int gpu;     // HIP device index or -1
-    int type;    // locale type (hclib_add_known_locale_type): 0 "sysmem", 1 "GPU"
-};
 
 // finish_t, src/inc/hclib-finish.h:6-10
 struct Finish {
@@ -48,6 +45,7 @@ struct hclib_task_t {
     std::vector<hclib_future_t *> *extra;
     int waiting_on_index;
     int device_kind;  // 0 = host task
+    int non_blocking; // hclib_async_nb (src/hclib.c:51-57)
     hclib_task_t *next_waiter;
 };
 
@@ -63,8 +61,13 @@ struct Runtime {
     std::vector<hclib_task_t *> ready;  // LIFO, like the owner end of a deque
     std::map<generic_frame_ptr, int> kinds;
     std::map<void *, int> bodies;
-    hclib_locale_t host{0, -1, 0};
-    hclib_locale_t gpu{1, 0, 1};
+    // [0] = the host ("sysmem"), [1] = this process's GPU ("GPU"): one array,
+    // as hclib_get_all_locales hands it out
+    hclib_locale_t locales[2] = {{0, 0, "sysmem", "sysmem", nullptr, nullptr, 0, 1, nullptr},
+                                 {1, 1, "GPU0", "GPU", nullptr, nullptr, 0, 1, nullptr}};
+    hclib_locale_t &host = locales[0];
+    hclib_locale_t &gpu = locales[1];
+    int gpu_index = 0;
     // locale types and their memory callbacks (src/hclib-mem.c:13-50)
     std::vector<std::string> types{"sysmem", "GPU"};
     struct MemFuncs {
@@ -235,7 +238,8 @@ bool run_one() {
     return true;
 }
 
-void spawn(generic_frame_ptr fp, void *arg, hclib_future_t **futures, int nfutures) {
+void spawn(generic_frame_ptr fp, void *arg, hclib_future_t **futures, int nfutures,
+           int non_blocking = 0) {
     Runtime &R = rt();
     if (!R.launched) die("hclib_async called outside hclib_launch");
     hclib_task_t *t = (hclib_task_t *)calloc(1, sizeof(hclib_task_t));
@@ -244,6 +248,7 @@ void spawn(generic_frame_ptr fp, void *arg, hclib_future_t **futures, int nfutur
     t->args = arg;
     auto k = R.kinds.find(fp);
     t->device_kind = (k == R.kinds.end()) ? 0 : k->second;
+    t->non_blocking = non_blocking;
     t->finish = R.current;
     check_in(t->finish);
     t->waiting_on_index = -1;
@@ -254,6 +259,29 @@ void spawn(generic_frame_ptr fp, void *arg, hclib_future_t **futures, int nfutur
     if (nfutures == 0 || register_all(t)) make_ready(t);
 }
 
+}  // namespace
+
+namespace {
+struct RootTask {
+    async_fct_t fn;
+    void *arg;
+    void *stack;
+};
+constexpr size_t kRootStack = 8u << 20;  // touched lazily
+ucontext_t g_root_ret, g_root_ctx;
+RootTask *g_root = nullptr;
+void root_trampoline() { g_root->fn(g_root->arg); }
+void run_root_on_own_stack(void *raw) {
+    RootTask *r = (RootTask *)raw;
+    r->stack = malloc(kRootStack);
+    if (!r->stack || getcontext(&g_root_ctx) != 0) die("hclib_launch: cannot create the root context");
+    g_root_ctx.uc_stack.ss_sp = r->stack;
+    g_root_ctx.uc_stack.ss_size = kRootStack;
+    g_root_ctx.uc_link = &g_root_ret;
+    g_root = r;
+    makecontext(&g_root_ctx, root_trampoline, 0);
+    if (swapcontext(&g_root_ret, &g_root_ctx) != 0) die("hclib_launch: cannot enter the root context");
+}
 }  // namespace
 
 extern "C" {
@@ -301,8 +329,14 @@ void hclib_launch(async_fct_t fct_ptr, void *arg, const char **deps, int ndeps) 
     const char *prof = getenv("HCLIB_PROFILE_LAUNCH_BODY");
     hclib_init(deps, ndeps, 0);
     const unsigned long long t0 = hclib_current_time_ns();
-    hclib_async(fct_ptr, arg, nullptr, 0, nullptr);  // src/hclib-runtime.c:1472
+    // the root task runs on a context of its own, as the reference's does
+    // (a LiteCtx fiber, src/hclib-runtime.c:1460-1478); its stack stays
+    // mapped until the launch ends, so tasks that outlive the root body and
+    // still read its locals (test/cpp/promise/future5.cpp) see them intact
+    RootTask root{fct_ptr, arg, nullptr};
+    hclib_async(run_root_on_own_stack, &root, nullptr, 0, nullptr);
     hclib_finalize(0);  // ends the root finish: the root task runs here
+    free(root.stack);
     const unsigned long long t1 = hclib_current_time_ns();
     if (prof && *prof) printf("\nHCLIB TIME %llu ns\n", t1 - t0);
 }
@@ -323,7 +357,23 @@ void hclib_async(generic_frame_ptr fp, void *arg, hclib_future_t **futures, cons
 }
 
 void hclib_async_nb(generic_frame_ptr fp, void *arg, hclib_locale_t *locale) {
-    hclib_async(fp, arg, nullptr, 0, locale);
+    (void)locale;
+    spawn(fp, arg, nullptr, 0, 1);
+}
+
+// hclib_yield, src/hclib-runtime.c:1142-1217, with the control thread as the
+// only host worker: run ready tasks, newest first, until none is left or a
+// blocking one has run (the reference breaks after it swaps to a blocking
+// task's context).
+void hclib_yield(hclib_locale_t *locale) {
+    (void)locale;
+    Runtime &R = rt();
+    if (!R.launched) die("hclib_yield called outside hclib_launch");
+    while (!R.ready.empty()) {
+        const int nb = R.ready.back()->non_blocking;
+        run_one();
+        if (!nb) break;
+    }
 }
 
 namespace {
@@ -391,14 +441,89 @@ hclib_future_t *hclib_end_finish_nonblocking(void) {
     return &e->future;
 }
 
+}  // extern "C"
+
+namespace {
+
+// A host loop body (a C function pointer the GPU cannot run) is lowered the
+// way the reference lowers every forasync (src/hclib.c:110-473): one task
+// per tile, registered with the enclosing finish, each running
+// forasync{1,2,3}D_runner's loop nest over its tile. The tiles are the runs
+// of include/hclib_forasync_sets.h, so the iteration set (including the
+// FLAT low != 0 overrun quirk) is the reference's.
+struct HostTile {
+    void *fct;
+    void *argv;
+    int dim;
+    hclib_sets::Run r[3];
+};
+
+void host_tile_runner(void *raw) {  // forasync{1,2,3}D_runner, src/hclib.c:110-156
+    HostTile *t = (HostTile *)raw;
+    const hclib_sets::Run &a = t->r[0], &b = t->r[1], &c = t->r[2];
+    for (int i = 0; i < a.count; ++i) {
+        const int x = a.first + i * a.stride;
+        if (t->dim == 1) {
+            ((forasync1D_Fct_t)t->fct)(t->argv, x);
+            continue;
+        }
+        for (int j = 0; j < b.count; ++j) {
+            const int y = b.first + j * b.stride;
+            if (t->dim == 2) {
+                ((forasync2D_Fct_t)t->fct)(t->argv, x, y);
+                continue;
+            }
+            for (int k = 0; k < c.count; ++k)
+                ((forasync3D_Fct_t)t->fct)(t->argv, x, y, c.first + k * c.stride);
+        }
+    }
+    free(t);
+}
+
+void forasync_host(void *fct, void *argv, int dim, hclib_loop_domain_t *domain, int mode) {
+    Runtime &R = rt();
+    R.forasyncs++;
+    std::vector<hclib_sets::Run> runs[3];
+    for (int d = 0; d < dim; ++d) {
+        if (domain[d].stride < 1) die("hclib_forasync: stride must be >= 1");
+        // tile == -1 -> auto, written back (src/hclib.c:455-461)
+        hclib_sets::resolve_tile(&domain[d].tile, domain[d].low, domain[d].high,
+                                 hclib_get_num_workers());
+        const hclib_sets::Domain dd{domain[d].low, domain[d].high, domain[d].stride, domain[d].tile};
+        runs[d] = hclib_sets::runs(dd, dim, mode == FORASYNC_MODE_RECURSIVE ? 1 : 0);
+    }
+    const hclib_sets::Run one{0, 1, 1, 0};
+    const size_t n1 = dim > 1 ? runs[1].size() : 1, n2 = dim > 2 ? runs[2].size() : 1;
+    for (const hclib_sets::Run &a : runs[0])
+        for (size_t j = 0; j < n1; ++j)
+            for (size_t k = 0; k < n2; ++k) {
+                HostTile *t = (HostTile *)malloc(sizeof(HostTile));
+                if (!t) die("out of memory");
+                t->fct = fct;
+                t->argv = argv;
+                t->dim = dim;
+                t->r[0] = a;
+                t->r[1] = dim > 1 ? runs[1][j] : one;
+                t->r[2] = dim > 2 ? runs[2][k] : one;
+                spawn(host_tile_runner, t, nullptr, 0);
+            }
+}
+
+}  // namespace
+
+extern "C" {
+
 // ------------------------------------------------------------- forasync
 void hclib_forasync(void *fct, void *argv, int dim, hclib_loop_domain_t *domain,
                     forasync_mode_t mode) {
     Runtime &R = rt();
+    if (!R.launched) die("hclib_forasync called outside hclib_launch");
+    if (dim < 1 || dim > 3) die("hclib_forasync: dim %d not in 1..3", dim);
     auto b = R.bodies.find(fct);
-    if (b == R.bodies.end())
-        die("hclib_forasync: %p is not a registered device loop body "
-            "(hclib_hip_register_forasync_body); forasync runs on the GPU only", fct);
+    if (b == R.bodies.end()) {  // a host loop body: host tile tasks
+        forasync_host(fct, argv, dim, domain, mode);
+        return;
+    }
     ensure_gpu("hclib_forasync");
     R.forasyncs++;
     static_assert(sizeof(hclib_loop_domain_t) == sizeof(hclib_hip_loop_domain_t), "layout");
@@ -658,13 +783,22 @@ hclib_locale_t *hclib_get_locale(int index) {
     return nullptr;
 }
 
+hclib_locale_t *hclib_get_all_locales(void) { return rt().locales; }
+
+int hclib_get_num_locales_of_type(int type) {
+    int n = 0;
+    hclib_locale_t **v = hclib_get_all_locales_of_type(type, &n);
+    free(v);
+    return n;
+}
+
 hclib_locale_t **hclib_get_all_locales_of_type(int type, int *out_count) {
     const int n = hclib_get_num_locales();
     hclib_locale_t **v = (hclib_locale_t **)malloc(sizeof(hclib_locale_t *) * (size_t)(n + 1));
     int k = 0;
     for (int i = 0; i < n; ++i) {
         hclib_locale_t *l = hclib_get_locale(i);
-        if (l && l->type == type) v[k++] = l;
+        if (l && (int)l->type == type) v[k++] = l;
     }
     if (out_count) *out_count = k;
     return v;
@@ -757,7 +891,7 @@ int hclib_get_current_worker(void) { return 0; }
 hclib_locale_t *hclib_get_closest_locale(void) { return &rt().host; }
 
 hclib_locale_t *hclib_hip_gpu_locale(int index) {
-    rt().gpu.gpu = index;
+    rt().gpu_index = index;
     return &rt().gpu;
 }
 

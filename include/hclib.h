@@ -27,14 +27,28 @@
  * async/finish/promise traffic runs on device counters; hclib_forasync of a
  * device body becomes one grid-stride launch. Other functions are host
  * tasks: they run on the control thread, help-first inside end_finish, as
- * the reference's help_finish does (src/hclib-runtime.c:1067-1119).
+ * the reference's help_finish does (src/hclib-runtime.c:1067-1119); a
+ * forasync of a host loop body becomes one host task per tile of the
+ * reference's FLAT/RECURSIVE lowering (src/hclib.c:110-473).
  * Errors abort with a message, like the reference's HASSERT/exit paths.
  */
 #ifndef HCLIB_H_
 #define HCLIB_H_
 
+#include <assert.h>
 #include <stddef.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* default async arguments, inc/hclib_common.h:10-22 (the reference's hclib.h
+ * pulls these and <stdlib.h>/<string.h>/<assert.h> in for its test programs) */
+#define NO_PROP 0
+#define NO_ARG NULL
+#define NO_DATUM NULL
+#define NO_FUTURE NULL
+#define ANY_PLACE NULL
+#define NO_ACCUM NULL
 
 #ifdef __cplusplus
 extern "C" {
@@ -67,7 +81,19 @@ typedef struct {
     int tile;
 } hclib_loop_domain_t;
 
-typedef struct hclib_locale_t hclib_locale_t; /* opaque */
+/* the reference's locale record, inc/hclib-locality-graph.h:56-67 (programs
+ * index hclib_get_all_locales() as an array, test/c/memory/allocate.c:42-47) */
+typedef struct _hclib_locale_t {
+    int id;
+    unsigned type;
+    const char *lbl;
+    const char *special_type;
+    void *metadata;
+    void (**idle_funcs)(void);
+    unsigned n_idle_funcs;
+    int reachable;
+    struct _hclib_deque_t *deques;
+} hclib_locale_t;
 
 typedef int forasync_mode_t;
 #define FORASYNC_MODE_RECURSIVE 1
@@ -116,6 +142,10 @@ int hclib_future_is_satisfied(hclib_future_t *future);
 
 /* ------------------------------------------------------------ queries */
 int hclib_get_num_workers(void);
+/* run ready tasks from the control thread before continuing
+ * (src/hclib-runtime.c:1142-1217: non-blocking tasks until none is left,
+ * a blocking one ends the yield) */
+void hclib_yield(hclib_locale_t *locale);
 int hclib_get_current_worker(void);
 hclib_locale_t *hclib_get_closest_locale(void);
 void hclib_print_runtime_stats(FILE *fp);
@@ -152,6 +182,8 @@ int hclib_get_locale_type(hclib_locale_t *locale);
 const char *hclib_get_locale_type_name(int type);
 int hclib_get_num_locales(void);
 hclib_locale_t *hclib_get_locale(int index); /* 0 = host, 1.. = GPUs */
+hclib_locale_t *hclib_get_all_locales(void);  /* contiguous, hclib_get_num_locales() long */
+int hclib_get_num_locales_of_type(int locale_type);
 hclib_locale_t **hclib_get_all_locales_of_type(int type, int *out_count); /* malloc'd */
 
 void hclib_register_alloc_func(int locale_type, hclib_module_alloc_impl_func_type func);

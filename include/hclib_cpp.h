@@ -171,6 +171,15 @@ inline void launch(const int nworkers, const char **deps, int ndeps, T &&lambda)
 inline int get_current_worker() { return hclib_get_current_worker(); }
 inline int get_num_workers() { return hclib_get_num_workers(); }
 inline locale_t *get_closest_locale() { return hclib_get_closest_locale(); }
+// inc/hclib_cpp.h:53-57
+inline int get_num_locales() { return hclib_get_num_locales(); }
+inline locale_t *get_all_locales() { return hclib_get_all_locales(); }
+inline locale_t **get_all_locales_of_type(int type, int *out_count) {
+    return hclib_get_all_locales_of_type(type, out_count);
+}
+// inc/hclib-async.h:564-571
+inline void yield() { hclib_yield(NULL); }
+inline void yield_at(locale_t *locale) { hclib_yield(locale); }
 inline unsigned long long current_time_ns() { return hclib_current_time_ns(); }
 
 // --------------------------------------------------------------- async
@@ -275,6 +284,24 @@ inline auto async_future_await(T &&lambda, std::vector<hclib_future_t *> &future
     -> future_t<decltype(lambda())> * {
     return detail::async_future_helper(std::forward<T>(lambda), futures.data(), (int)futures.size(),
                                        nullptr);
+}
+
+// inc/hclib-async.h:515-547
+template <typename T>
+inline auto async_future_await_at(T &&lambda, hclib_future_t *f, hclib_locale_t *locale)
+    -> future_t<decltype(lambda())> * {
+    hclib_future_t *fs[1] = {f};
+    return detail::async_future_helper(std::forward<T>(lambda), f ? fs : nullptr, f ? 1 : 0, locale);
+}
+template <typename T>
+inline auto async_future_await_at(T &&lambda, std::vector<hclib_future_t *> &futures, hclib_locale_t *locale)
+    -> future_t<decltype(lambda())> * {
+    return detail::async_future_helper(std::forward<T>(lambda), futures.data(), (int)futures.size(), locale);
+}
+template <typename T>
+inline auto async_future_await_at(T &&lambda, std::vector<hclib_future_t *> &&futures, hclib_locale_t *locale)
+    -> future_t<decltype(lambda())> * {
+    return detail::async_future_helper(std::forward<T>(lambda), futures.data(), (int)futures.size(), locale);
 }
 
 // ------------------------------------------------------ memory at locales
