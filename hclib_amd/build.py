@@ -26,7 +26,7 @@ LIB = os.path.join(OUT, "libhclib_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["module.hip", "forasync.hip", "uts.hip", "fib.hip", "sw.hip", "hclib_api.hip", "calib.hip"]
+SOURCES = ["module.hip", "forasync.hip", "uts.hip", "fib.hip", "sw.hip", "dag.hip", "hclib_api.hip", "calib.hip"]
 CFLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
     "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result",

@@ -228,6 +228,43 @@ typedef struct {
  * (continuation by the last arriver). n <= 80. */
 int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *result);
 
+/* ---------------------------------------------- device promise DAG */
+/* Device promises/futures with dependency-counter release
+ * (include/hclib_hip/hx_dag.h; replaces hclib_promise_put's waiter walk,
+ * src/hclib-promise.c:132-245, and spawn_await, src/hclib-runtime.c:596-644,
+ * for device tasks). The caller describes `ntasks` tasks, each with
+ * `payload_words` u32 of payload and the promises it awaits (CSR:
+ * await_off[ntasks + 1], await_ids), and the promises already put before the
+ * launch (preput[p] != 0, their datum in preput_datum; either may be NULL).
+ * begin() uploads the graph, sizes every task's dependency counter, seeds
+ * the ready list with the tasks that wait on nothing and records the start
+ * event; the caller launches `grid` workgroups of 64 threads on `stream`
+ * running hx::run_dag_worker<Kind> over `view` (hclib::hip::run_dag does
+ * both); end() waits, copies each promise's datum / satisfied flag back
+ * (either output may be NULL) and returns HCLIB_HIP_EDEVICE for a double put
+ * or a task nothing releases (bounded spin, the reference's end_finish
+ * deadlock). */
+typedef struct {
+    void *view;        /* hx::DagView (device pointers, by value) */
+    void *stream;      /* hipStream_t of the module */
+    int grid;          /* workgroups (waves) to launch */
+    uint32_t ntasks, npromises;
+} hclib_hip_dag_launch_t;
+
+typedef struct {
+    uint64_t tasks;      /* tasks executed */
+    uint64_t puts;       /* device puts */
+    uint64_t releases;   /* counter decrements that made a task ready */
+    double kernel_ms;
+} hclib_hip_dag_stats_t;
+
+int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t payload_words,
+                        const uint32_t *payload, const uint32_t *await_off, const uint32_t *await_ids,
+                        const uint8_t *preput, const uint64_t *preput_datum, int waves_per_cu,
+                        uint32_t spin_limit_ms, hclib_hip_dag_launch_t *out);
+int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *satisfied_out,
+                      hclib_hip_dag_stats_t *stats);
+
 /* ---------------------------------------------------------------- SW */
 typedef struct {
     uint64_t tiles;      /* tile tasks executed */

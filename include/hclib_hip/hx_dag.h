@@ -1,0 +1,145 @@
+// hx_dag.h — device promises, futures and dependency-counter task release.
+//
+// Replaces the reference's promise machinery for device tasks:
+//   hclib_promise_put            src/hclib-promise.c:203-245 (walk the waiter
+//                                list, re-register or schedule each waiter)
+//   register_on_all_promise_dependencies / _register_if_promise_not_ready
+//                                src/hclib-promise.c:132-195 (a task parks on
+//                                its first unsatisfied future)
+//   spawn_await / async_await    src/hclib-runtime.c:596-644,
+//                                inc/hclib-async.h:247-355
+// with one counter per task instead of a parking chain: the host sizes each
+// task's counter to the number of its futures whose promises are not yet
+// satisfied and builds, per promise, the list of tasks awaiting it (a CSR).
+// A device put publishes the datum, marks the promise satisfied (a second put
+// is the reference's "single assignment" HASSERT, here a device error), and
+// decrements every waiter's counter — lanes in parallel; the decrement that
+// reaches zero appends the waiter to a ticket-ordered ready list. Persistent
+// waves take tickets in order (one agent atomic each) and run the task
+// (Kind::run, a wave-wide body). The DAG is acyclic and every ticket below
+// the task count is eventually filled, so waits end; a task whose promise
+// nobody puts is reported as a bounded-spin timeout, the reference's
+// end_finish deadlock.
+//
+// Memory protocol (hx_common.h, MI355X_MICROARCH.md "Valid forms"): a put
+// releases at agent scope first (the body's plain stores become visible),
+// stores the datum write-through and drains it before any decrement; a wave
+// acquires at agent scope before running a task it took from the list.
+#pragma once
+
+#include "hx_common.h"
+
+namespace hx {
+
+constexpr uint32_t kDagEmpty = 0xffffffffu;
+
+enum : uint32_t { kErrDoublePut = 7 };
+
+// Device view of one DAG launch (hclib_hip_dag_launch_t, include/hclib_hip.h).
+struct DagView {
+    uint32_t *deps;              // [ntasks] unsatisfied futures per task
+    const uint32_t *waiter_off;  // [npromises + 1] CSR offsets
+    const uint32_t *waiters;     // tasks awaiting each promise (a task once per await)
+    unsigned long long *datum;   // [npromises]
+    uint32_t *satisfied;         // [npromises]
+    const uint32_t *payload;     // [ntasks * payload_words]
+    uint32_t *ready;             // [ntasks] ticket-ordered ready list
+    uint32_t *head;              // next ticket
+    uint32_t *tail;              // next free ready slot
+    uint32_t *err;               // DevError
+    unsigned long long *stats;   // [0] tasks run, [1] puts, [2] releases
+    uint32_t ntasks, npromises, payload_words, spin_ms;
+};
+
+// Per-wave state a task body receives: the view and the wave's counters.
+struct DagWave {
+    DagView v;
+    unsigned long long puts, releases;
+};
+
+// hclib_future_get on the device: the datum of a satisfied promise (one the
+// running task awaited, or one put before the launch).
+__device__ __forceinline__ unsigned long long dag_get(const DagWave &w, uint32_t p) {
+    return ld_agent(&w.v.datum[p]);
+}
+
+__device__ __forceinline__ bool dag_is_satisfied(const DagWave &w, uint32_t p) {
+    return ld_agent(&w.v.satisfied[p]) != 0;
+}
+
+// hclib_promise_put on the device. Wave-uniform: every lane calls it with the
+// same (p, datum); lanes share the waiter decrements.
+__device__ __forceinline__ void dag_put(DagWave &w, uint32_t p, unsigned long long datum) {
+    const DagView &v = w.v;
+    const int lane = lane_id();
+    release_agent();
+    uint32_t was = 0;
+    if (lane == 0) {
+        st_agent(&v.datum[p], datum);
+        was = __hip_atomic_exchange(&v.satisfied[p], 1u, __ATOMIC_RELAXED, HX_AGENT);
+    }
+    was = (uint32_t)__shfl((int)was, 0, 64);
+    if (was) {  // src/hclib-promise.c:206-207
+        if (lane == 0) dev_error(v.err, kErrDoublePut);
+        return;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the datum lands before any release
+    const uint32_t b = v.waiter_off[p], e = v.waiter_off[p + 1];
+    uint32_t rel = 0;
+    for (uint32_t k = b + (uint32_t)lane; k < e; k += 64) {
+        const uint32_t t = v.waiters[k];
+        if (add_agent(&v.deps[t], (uint32_t)-1) == 1u) {
+            const uint32_t pos = add_agent(v.tail, 1u);
+            st_agent(&v.ready[pos], t);
+            ++rel;
+        }
+    }
+    w.puts += 1;
+    w.releases += (unsigned long long)wave_sum((int)rel);
+}
+
+// Kind concept:
+//   struct Ctx;   // per-launch parameters (passed by value)
+//   __device__ static void run(const Ctx&, DagWave&, uint32_t task,
+//                              const uint32_t *payload);
+//        a wave-wide body: every lane enters; dag_get reads the futures it
+//        awaited, dag_put satisfies promises (wave-uniform calls).
+template <class Kind>
+__device__ void run_dag_worker(const typename Kind::Ctx &ctx, const DagView &view) {
+    DagWave w{view, 0, 0};
+    const int lane = lane_id();
+    unsigned long long ran = 0;
+    while (true) {
+        uint32_t ticket = 0;
+        if (lane == 0) ticket = add_agent(view.head, 1u);
+        ticket = (uint32_t)__shfl((int)ticket, 0, 64);
+        if (ticket >= view.ntasks) break;
+        uint32_t t = kDagEmpty;
+        if (lane == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while ((t = ld_agent(&view.ready[ticket])) == kDagEmpty) {
+                if (ld_agent(view.err)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * view.spin_ms) {
+                    dev_error(view.err, kErrSpinTimeout);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        t = (uint32_t)__shfl((int)t, 0, 64);
+        if (t == kDagEmpty || t >= view.ntasks) {
+            if (t != kDagEmpty && lane == 0) dev_error(view.err, kErrBadTask);
+            break;
+        }
+        acquire_agent();
+        Kind::run(ctx, w, t, view.payload + (size_t)t * view.payload_words);
+        ++ran;
+    }
+    if (lane == 0) {
+        add_agent(&view.stats[0], ran);
+        add_agent(&view.stats[1], w.puts);
+        add_agent(&view.stats[2], w.releases);
+    }
+}
+
+}  // namespace hx

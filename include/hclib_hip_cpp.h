@@ -13,6 +13,15 @@
  *       (include/hclib_forasync_sets.h). Blocking, like the reference's
  *       finish-wrapped forasync; the _nb forms return after enqueueing.
  *
+ *   hclib::hip::dag + run_dag<Kind>(ctx, graph, &stats)
+ *       hclib::promise_t / async_await for device tasks: the host declares
+ *       promises and tasks (each with a payload and the futures it awaits,
+ *       inc/hclib-async.h:247-355); one persistent launch runs the graph,
+ *       task bodies read futures with hx::dag_get and satisfy promises with
+ *       hx::dag_put, which releases waiters through dependency counters
+ *       (include/hclib_hip/hx_dag.h). Blocking, like a finish around the
+ *       asyncs; afterwards graph.datum(p) is each promise's value.
+ *
  *   hclib::hip::run_tasks<Kind>(ctx, &stats)
  *       a user-defined device task kind on the persistent work-stealing
  *       megakernel (include/hclib_hip/hx_sched.h): the GPU form of
@@ -30,10 +39,12 @@
 
 #include <hip/hip_runtime.h>
 
+#include <initializer_list>
 #include <vector>
 
 #include "hclib_cpp.h"
 #include "hclib_hip.h"
+#include "hclib_hip/hx_dag.h"
 #include "hclib_hip/hx_sched.h"
 
 namespace hclib {
@@ -240,6 +251,82 @@ int run_tasks(const typename Kind::Ctx &ctx, task_stats *stats = nullptr, const 
     task_stats local;
     task_stats *s = stats ? stats : &local;
     return hclib_hip_sched_end("hclib::hip::run_tasks", s->counters, s->maxes, &s->kernel_ms);
+}
+
+// ------------------------------------------------ device promise DAG
+class dag;
+// Run every task of `g` on the GPU and wait (the enclosing finish ends).
+// Errors: a double put or a task nothing releases -> HCLIB_HIP_EDEVICE.
+template <class Kind>
+int run_dag(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats = nullptr, int waves_per_cu = 4,
+            uint32_t spin_limit_ms = 0);
+
+// Host-side graph builder: the device counterpart of creating promises with
+// hclib_promise_create and tasks with hclib_async(fn, arg, futures, n).
+class dag {
+  public:
+    explicit dag(uint32_t payload_words) : words_(payload_words) { await_off_.push_back(0); }
+
+    // hclib_promise_create: a new promise id
+    uint32_t promise() {
+        preput_.push_back(0);
+        pre_datum_.push_back(0);
+        return (uint32_t)preput_.size() - 1;
+    }
+    // hclib_promise_put before the launch (e.g. the boundary promises of
+    // test/smithwaterman/smith_waterman.cpp:141-165)
+    void put(uint32_t p, uint64_t datum) {
+        preput_.at(p) = 1;
+        pre_datum_.at(p) = datum;
+    }
+    // hclib_async(..., futures, n): a task with `payload_words` words of
+    // payload that runs once every awaited promise is put
+    uint32_t async_await(const uint32_t *payload, const uint32_t *futures, int n) {
+        payload_.insert(payload_.end(), payload, payload + words_);
+        for (int i = 0; i < n; ++i) await_ids_.push_back(futures[i]);
+        await_off_.push_back((uint32_t)await_ids_.size());
+        return (uint32_t)await_off_.size() - 2;
+    }
+    uint32_t async_await(const uint32_t *payload, std::initializer_list<uint32_t> futures) {
+        std::vector<uint32_t> f(futures);
+        return async_await(payload, f.data(), (int)f.size());
+    }
+    uint32_t num_tasks() const { return (uint32_t)await_off_.size() - 1; }
+    uint32_t num_promises() const { return (uint32_t)preput_.size(); }
+    // after run_dag: hclib_future_get / hclib_future_is_satisfied
+    uint64_t datum(uint32_t p) const { return datum_.at(p); }
+    bool satisfied(uint32_t p) const { return sat_.at(p) != 0; }
+
+    template <class Kind>
+    friend int run_dag(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats, int waves_per_cu,
+                       uint32_t spin_limit_ms);
+
+  private:
+    uint32_t words_;
+    std::vector<uint32_t> payload_, await_off_, await_ids_;
+    std::vector<uint8_t> preput_, sat_;
+    std::vector<uint64_t> pre_datum_, datum_;
+};
+
+template <class Kind>
+__global__ __launch_bounds__(64) void k_run_dag(typename Kind::Ctx ctx, hx::DagView v) {
+    hx::run_dag_worker<Kind>(ctx, v);
+}
+
+template <class Kind>
+int run_dag(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats, int waves_per_cu,
+            uint32_t spin_limit_ms) {
+    hclib_hip_dag_launch_t L;
+    int rc = hclib_hip_dag_begin(g.num_tasks(), g.num_promises(), g.words_, g.payload_.data(), g.await_off_.data(),
+                                 g.await_ids_.data(), g.preput_.data(), g.pre_datum_.data(), waves_per_cu,
+                                 spin_limit_ms, &L);
+    if (rc != HCLIB_HIP_OK) return rc;
+    const hx::DagView v = *(const hx::DagView *)L.view;
+    hipLaunchKernelGGL((k_run_dag<Kind>), dim3(L.grid), dim3(64), 0, (hipStream_t)L.stream, ctx, v);
+    g.datum_.assign(g.num_promises(), 0);
+    g.sat_.assign(g.num_promises(), 0);
+    hclib_hip_dag_stats_t local;
+    return hclib_hip_dag_end("hclib::hip::run_dag", g.datum_.data(), g.sat_.data(), stats ? stats : &local);
 }
 
 }  // namespace hip

@@ -33,3 +33,23 @@ def test_device_api_on_gpu():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Check results: OK" in r.stdout
     assert "fib(25) = 75025" in r.stdout and "queens(12) = 14200 solutions" in r.stdout
+
+
+DAG_EXE = os.path.join(os.path.dirname(H.LIB_PATH), "tests", "device_dag")
+
+
+def test_device_dag_program_is_built():
+    assert os.path.exists(DAG_EXE), "run python -m hclib_amd.build"
+
+
+@pytest.mark.gpu
+def test_device_promise_dag_on_gpu():
+    """Device promises/futures with dependency-counter release
+    (include/hclib_hip/hx_dag.h): chain, SW-style wavefront with plain-data
+    hand-offs, random DAG with > MAX_NUM_WAITS futures, 30,000-way fan-out,
+    all bit-exact against serial host evaluation; a double put and an
+    unsatisfiable future return HCLIB_HIP_EDEVICE instead of hanging."""
+    r = subprocess.run([DAG_EXE], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Check results: OK" in r.stdout
+    assert "single assignment" in r.stdout and "deadlock" in r.stdout
