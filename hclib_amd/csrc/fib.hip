@@ -157,6 +157,7 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_FIB_HUNGER", 8);
+    cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 1);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     hipLaunchKernelGGL(k_fib, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);

@@ -537,6 +537,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", 8);
+    cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 1);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     const bool feat = nshards > 1 || max_levels > 0;

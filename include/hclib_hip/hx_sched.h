@@ -111,6 +111,9 @@ struct SchedConfig {
     uint32_t stamps;     // diagnostic: accumulate per-phase s_memtime cycles
     uint32_t hunger;     // batches between reads of the hunger signal (0: never give work
                          // away unless the ring is full)
+    uint32_t carry = 1;  // keep a uniform batch's outputs in registers as the next batch
+                         // (no ring push / pop) while they fit one batch and no hungry
+                         // wave could take them (see run_worker)
 };
 
 // Kind concept:
@@ -440,6 +443,13 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     unsigned long long cyc_busy = 0, cyc_idle = 0, cyc_spill = 0, cyc_form = 0, cyc_proc = 0, cyc_push = 0;
     uint32_t tag = 1;  // mark tags: 16 per batch
     for (int i = lane; i < kWaveSize; i += kWaveSize) st.mark[i] = 0;
+    // register carry: the previous batch's `carry` outputs, lane o holding
+    // item o (template ctmpl, child index ck); they form the front of the
+    // next batch instead of round-tripping through the LDS ring
+    uint32_t carry = 0, ck = 0;
+    uint32_t ctmpl[TW];
+#pragma unroll
+    for (int i = 0; i < TW; ++i) ctmpl[i] = 0;
 
     if (seed_roots) {
         uint32_t tmpl[TW];
@@ -476,8 +486,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         // bookkeeping is scalar and its branches are s_cbranch_scc
         top = lane0(top);
         bot = lane0(bot);
+        carry = lane0(carry);
         const uint32_t size = top - bot;
-        if (size == 0) {
+        if (size == 0 && carry == 0) {
             if (busy_phase) {
                 const unsigned long long now = __builtin_amdgcn_s_memtime();
                 cyc_busy += now - t_mark;
@@ -555,21 +566,30 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             --hunger_in;
             outst = outst_cur;
         }
-        // ---- a batch = the top min(size, 64) items, one per lane
-        const uint32_t take = size < (uint32_t)kWaveSize ? size : (uint32_t)kWaveSize;
+        // ---- a batch = the carried items, then the top items of the ring,
+        // min(carry + size, 64) in all, one per lane
+        const uint32_t room = (uint32_t)kWaveSize - carry;
+        const uint32_t take_ring = size < room ? size : room;
+        const uint32_t take = carry + take_ring;
         const bool has = (uint32_t)lane < take;
         uint32_t tmpl[TW], child[TW];
         uint32_t k = 0, kend = 0;
         int cnt = 0;
         unsigned long long ts0 = 0;
         if (HX_STAMPS && cfg.stamps) ts0 = __builtin_amdgcn_s_memtime();
-        if (Kind::kPure || has) {  // pure kinds: every lane loads (slots wrap inside the ring)
-            const uint32_t p = top - 1 - (uint32_t)lane;
+        if ((uint32_t)lane < carry) {
+#pragma unroll
+            for (int i = 0; i < TW; ++i) tmpl[i] = ctmpl[i];
+            k = ck;
+            kend = ck + 1;
+        } else if (Kind::kPure || has) {  // pure kinds: every lane loads (slots wrap inside the ring)
+            const uint32_t p = top - 1 - ((uint32_t)lane - carry);
             const uint2 dd = st.d[p & M];
             k = dd.x;
             kend = has ? dd.y & (kMaxChildren - 1) : k + 1;
             load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & M, tmpl);
         }
+        carry = 0;
         unsigned long long tsl = 0;
         if (HX_STAMPS && cfg.stamps) {
             // diagnostic build only: form = loop top + pop (LDS loads landed)
@@ -587,7 +607,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
             cyc_proc += ts1 - tsl;
         }
-        top -= take;
+        top -= take_ring;
         // ---- push: residual range of the item + the new task's children
         const uint32_t rlen = has ? kend - k - 1u : 0u;
         const uint32_t nres = rlen == 0 ? 0u : (rlen == 1 ? 1u : 2u);
@@ -612,6 +632,35 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             const int P = wave_scan_add(nout);
             tout = (uint32_t)lane63(P);
             excl = (uint32_t)(P - nout);
+        }
+        // register carry: a uniform batch whose outputs fit one batch keeps
+        // them in registers as the front of the next batch — unless a hungry
+        // wave could be given items from the ring (then they go through it).
+        // Output o is child o % mu of the spawning lane of rank o / mu: one
+        // ds_permute tells rank r its source lane, two ds_bpermute hops bring
+        // the template to lane o.
+        {
+            const uint32_t hungry0 = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
+            if (cfg.carry && uniform && tout > 0 && tout <= (uint32_t)kWaveSize &&
+                !(hungry0 > 0 && (top - bot) + tout >= cfg.spill_lo)) {
+                const uint32_t nsp = (uint32_t)__builtin_popcountll(spawn);
+                const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(spawn >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
+                const uint32_t dst = nch != 0 ? rk : nsp + ((uint32_t)lane - rk);
+                const int src_of_rank = __builtin_amdgcn_ds_permute((int)(dst * 4u), lane);
+                const uint32_t rcp = (65536u + mu - 1) / mu;
+                const uint32_t o = (uint32_t)lane;
+                const uint32_t r = (o * rcp) >> 16;  // o / mu (o < 64, mu <= 8)
+                const int src = __builtin_amdgcn_ds_bpermute((int)(r * 4u), src_of_rank);
+#pragma unroll
+                for (int i = 0; i < TW; ++i)
+                    ctmpl[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(src * 4, (int)child[i]);
+                ck = o - r * mu;
+                carry = tout;
+                if (HX_STAMPS && cfg.stamps) cyc_push += __builtin_amdgcn_s_memtime() - ts0;
+                if (HX_STAMPS && cfg.stamps) t_batch = __builtin_amdgcn_s_memtime();
+                continue;
+            }
         }
         // a push that would come near live items first moves the oldest
         // items out as chunks (rare: only bursts of wide nodes)
