@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "hx_module.h"
+#include "../../include/hclib_hip/hx_dag.h"
 
 namespace hx {
 
@@ -468,6 +469,34 @@ __global__ __launch_bounds__(64) void k_sw_rows(SwCtx c) {
     }
 }
 
+// The generic device promise DAG (include/hclib_hip/hx_dag.h) driving the
+// reference's tile program as written: every tile is an async_await on three
+// futures (left tile's right column, up tile's bottom row, diagonal tile's
+// corner, smith_waterman.cpp:227-229) and puts three promises when done
+// (:212-226). The boundary promises the reference puts before the loop
+// (:141-165) are simply not awaited.
+struct SwDagKind {
+    using Ctx = SwCtx;
+    __device__ static void run(const SwCtx &c, DagWave &w, uint32_t t, const uint32_t *) {
+        extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+        int *lds_top = sw_lds;
+        int *lds_bot = sw_lds + ((c.tw + 1 + 3) & ~3);
+        int8_t *lds_s1 = (int8_t *)(lds_bot + ((c.tw + 1 + 3) & ~3) + 68);
+        unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+        int corner_unused = 0;
+        __syncthreads();
+        sw_tile<false>(c, t, lds_top, lds_bot, lds_s1, nullptr, nullptr, corner_unused, ph);
+        // the tile's outputs were stored write-through; the puts release them
+        dag_put(w, 3u * t + 0u, 0ull);                                    // right column
+        dag_put(w, 3u * t + 1u, 0ull);                                    // bottom row
+        dag_put(w, 3u * t + 2u, (unsigned long long)(uint32_t)ld_agent(&c.corner[t]));  // corner
+    }
+};
+
+__global__ __launch_bounds__(64) void k_sw_dag(SwCtx c, DagView v) {
+    run_dag_worker<SwDagKind>(c, v);
+}
+
 __global__ void k_sw_init(uint32_t *deps, uint32_t *ready, int ntw, int nth) {
     const uint32_t n = (uint32_t)(ntw * nth);
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
@@ -504,7 +533,8 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     // the row schedule keeps two tile columns in LDS: wide tiles fall back
     const size_t rows_lds = 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + 68 * 4 + 2 * (size_t)((tw + 3) & ~3) + 16 +
                             2 * (size_t)(((th + 3) & ~3) * 4);
-    const bool rows = !(sched && !strcmp(sched, "queue")) && rows_lds <= 64 * 1024;
+    const bool dag = sched && !strcmp(sched, "dag");
+    const bool rows = !(sched && (!strcmp(sched, "queue") || dag)) && rows_lds <= 64 * 1024;
     const size_t nt = ntw * nth;
     const size_t b_s1 = ntw * tw, b_s2 = nth * th;
     const size_t b_bot = rows ? 0 : nt * tw * 4, b_right = rows ? 0 : nt * th * 4, b_c = nt * 4,
@@ -562,13 +592,33 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     if (wpc < 1) wpc = 1;
     int grid = m.num_cus * wpc;
     if (rows && grid > (int)nth) grid = (int)nth;
-    const void *kern = rows ? (const void *)k_sw_rows : (const void *)k_sw;
+    const void *kern = rows ? (const void *)k_sw_rows : (dag ? (const void *)k_sw_dag : (const void *)k_sw);
     if (lds > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if ((rc = hip_check(hipEventRecord(m.ev0, m.stream), "event"))) return fail(rc);
-    if (rows) hipLaunchKernelGGL(k_sw_rows, dim3(grid), dim3(64), lds, m.stream, c);
-    else hipLaunchKernelGGL(k_sw, dim3(grid), dim3(64), lds, m.stream, c);
-    if ((rc = hip_check(hipGetLastError(), "k_sw launch"))) return fail(rc);
-    if ((rc = hip_check(hipEventRecord(m.ev1, m.stream), "event"))) return fail(rc);
+    hclib_hip_dag_stats_t dst{};
+    if (dag) {
+        // the tile program's futures as a CSR over 3 promises per tile
+        std::vector<uint32_t> off(nt + 1, 0), ids;
+        ids.reserve(3 * nt);
+        for (size_t t = 0; t < nt; ++t) {
+            const size_t i = t / ntw, j = t % ntw;
+            if (j > 0) ids.push_back((uint32_t)(3 * (t - 1) + 0));
+            if (i > 0) ids.push_back((uint32_t)(3 * (t - ntw) + 1));
+            if (i > 0 && j > 0) ids.push_back((uint32_t)(3 * (t - ntw - 1) + 2));
+            off[t + 1] = (uint32_t)ids.size();
+        }
+        hclib_hip_dag_launch_t L;
+        if ((rc = hclib_hip_dag_begin((uint32_t)nt, (uint32_t)(3 * nt), 0, nullptr, off.data(), ids.data(), nullptr,
+                                      nullptr, wpc, c.spin_ms, &L)))
+            return fail(rc);
+        hipLaunchKernelGGL(k_sw_dag, dim3(L.grid), dim3(64), lds, m.stream, c, *(const DagView *)L.view);
+        if ((rc = hclib_hip_dag_end("hclib_hip_sw (dag)", nullptr, nullptr, &dst))) return fail(rc);
+    } else {
+        if ((rc = hip_check(hipEventRecord(m.ev0, m.stream), "event"))) return fail(rc);
+        if (rows) hipLaunchKernelGGL(k_sw_rows, dim3(grid), dim3(64), lds, m.stream, c);
+        else hipLaunchKernelGGL(k_sw, dim3(grid), dim3(64), lds, m.stream, c);
+        if ((rc = hip_check(hipGetLastError(), "k_sw launch"))) return fail(rc);
+        if ((rc = hip_check(hipEventRecord(m.ev1, m.stream), "event"))) return fail(rc);
+    }
     uint32_t herr = 0;
     unsigned long long st[10] = {0};
     int corner = 0;
@@ -588,6 +638,10 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         st[1] = 3ull * (ntw - 1) * (nth - 1) + (ntw - 1) + (nth - 1);
     } else {
         (void)hipMemcpy(&corner, c.corner + (nt - 1), 4, hipMemcpyDeviceToHost);
+    }
+    if (dag) {  // the DAG's own counters: tasks run, and every future resolved
+        st[0] = dst.tasks;
+        st[1] = 3ull * (ntw - 1) * (nth - 1) + (ntw - 1) + (nth - 1);
     }
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);

@@ -234,6 +234,17 @@ def test_sw_64k_golden(golden):
     assert st["releases"] == 3 * 255 * 255 + 2 * 255
 
 
+def test_sw_64k_golden_on_generic_promise_dag(golden, monkeypatch):
+    """The 64K config as the reference writes it — 65,536 async_await tiles,
+    196,608 promises — through device promises/futures: score 128772."""
+    monkeypatch.setenv("HCLIB_HIP_SW_SCHED", "dag")
+    g = golden("sw_goldens.json")["sw64k"]
+    s1, s2 = _sw_inputs("huge")
+    score, st = H.sw(s1[:65536], s2[:65536], 256, 256)
+    assert score == g["score"] == 128772
+    assert st["tiles"] == 65536
+
+
 def test_sw_random_vs_oracle():
     rng = np.random.default_rng(5)
     for (n1, n2, tw, th) in [(300, 200, 17, 13), (1000, 777, 64, 300), (513, 1025, 256, 64)]:
@@ -243,11 +254,13 @@ def test_sw_random_vs_oracle():
         assert score == L.sw_score(s1, s2, tw, th)
 
 
-@pytest.mark.parametrize("sched", ["queue", "rows"])
+@pytest.mark.parametrize("sched", ["queue", "rows", "dag"])
 def test_sw_both_schedules(golden, sched, monkeypatch):
-    """The generic DAG schedule (device dependency counters + ready list) and
-    the row schedule (owner-computes tile rows, granule hand-offs) give the
-    published scores and the oracle's on ragged tile grids."""
+    """The tile-counter schedule (device dependency counters + ready list),
+    the row schedule (owner-computes tile rows, granule hand-offs) and the
+    reference's own promise program on the generic device DAG (3 futures, 3
+    puts per tile, include/hclib_hip/hx_dag.h) give the published scores and
+    the oracle's on ragged tile grids."""
     monkeypatch.setenv("HCLIB_HIP_SW_SCHED", sched)
     g = golden("sw_goldens.json")["published"]["large"]
     s1, s2 = _sw_inputs("large")
