@@ -259,6 +259,12 @@ def main():
         s2 = H.sw_map(open(os.path.join(ROOT, "tests/golden/sw/string2-huge.txt"), "rb").read())[:65536]
         score, swst = H.sw(s1, s2, 256, 256)
         assert score == 128772
+        # the same DAG as the reference writes it (3 futures / 3 puts per
+        # tile) on the generic device promise machinery
+        os.environ["HCLIB_HIP_SW_SCHED"] = "dag"
+        dscore, dagst = H.sw(s1, s2, 256, 256)
+        del os.environ["HCLIB_HIP_SW_SCHED"]
+        assert dscore == 128772
         out["configs"] = {
             "uts_t1_1gpu": {"nodes_per_s": T1_GOLD[0] / (t1["kernel_ms"] * 1e-3),
                             "kernel_ms": t1["kernel_ms"]},
@@ -267,6 +273,9 @@ def main():
                           "tasks": fst["tasks"], "kernel_ms": fst["kernel_ms"]},
             "sw_64k": {"cells_per_s": swst["cells_per_s"], "kernel_ms": swst["kernel_ms"],
                        "score": score},
+            "sw_64k_promise_dag": {"cells_per_s": dagst["cells_per_s"], "kernel_ms": dagst["kernel_ms"],
+                                   "tile_tasks_per_s": 65536 / (dagst["kernel_ms"] * 1e-3),
+                                   "score": dscore},
         }
         out["atomics"] = measure_atomics(H, fst)
         threads = int(os.environ.get("HCLIB_BENCH_CPU_THREADS",
