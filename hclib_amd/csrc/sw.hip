@@ -486,10 +486,10 @@ struct SwDagKind {
         int corner_unused = 0;
         __syncthreads();
         sw_tile<false>(c, t, lds_top, lds_bot, lds_s1, nullptr, nullptr, corner_unused, ph);
-        // the tile's outputs were stored write-through; the puts release them
-        dag_put(w, 3u * t + 0u, 0ull);                                    // right column
-        dag_put(w, 3u * t + 1u, 0ull);                                    // bottom row
-        dag_put(w, 3u * t + 2u, (unsigned long long)(uint32_t)ld_agent(&c.corner[t]));  // corner
+        // right column, bottom row, corner (:212-226): one release for all three
+        const uint32_t ps[3] = {3u * t + 0u, 3u * t + 1u, 3u * t + 2u};
+        const unsigned long long ds[3] = {0ull, 0ull, (unsigned long long)(uint32_t)ld_agent(&c.corner[t])};
+        dag_put_n<3>(w, ps, ds);
     }
 };
 

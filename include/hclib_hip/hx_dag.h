@@ -67,24 +67,26 @@ __device__ __forceinline__ bool dag_is_satisfied(const DagWave &w, uint32_t p) {
     return ld_agent(&w.v.satisfied[p]) != 0;
 }
 
-// hclib_promise_put on the device. Wave-uniform: every lane calls it with the
-// same (p, datum); lanes share the waiter decrements.
-__device__ __forceinline__ void dag_put(DagWave &w, uint32_t p, unsigned long long datum) {
+// One promise of a put: publish the datum, mark it satisfied and release its
+// waiters. The datum store, the satisfied exchange and the waiter-range loads
+// are in flight together (one memory round trip before the decrements); a
+// second put on a satisfied promise is reported as kErrDoublePut (its stray
+// decrements only move counters already at zero, which never release).
+__device__ __forceinline__ void dag_put_one(DagWave &w, uint32_t p, unsigned long long datum) {
     const DagView &v = w.v;
     const int lane = lane_id();
-    release_agent();
+    const uint32_t b = v.waiter_off[p], e = v.waiter_off[p + 1];
     uint32_t was = 0;
     if (lane == 0) {
         st_agent(&v.datum[p], datum);
         was = __hip_atomic_exchange(&v.satisfied[p], 1u, __ATOMIC_RELAXED, HX_AGENT);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the datum lands before any release
     was = (uint32_t)__shfl((int)was, 0, 64);
     if (was) {  // src/hclib-promise.c:206-207
         if (lane == 0) dev_error(v.err, kErrDoublePut);
         return;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the datum lands before any release
-    const uint32_t b = v.waiter_off[p], e = v.waiter_off[p + 1];
     uint32_t rel = 0;
     for (uint32_t k = b + (uint32_t)lane; k < e; k += 64) {
         const uint32_t t = v.waiters[k];
@@ -96,6 +98,23 @@ __device__ __forceinline__ void dag_put(DagWave &w, uint32_t p, unsigned long lo
     }
     w.puts += 1;
     w.releases += (unsigned long long)wave_sum((int)rel);
+}
+
+// hclib_promise_put on the device. Wave-uniform: every lane calls it with the
+// same (p, datum); lanes share the waiter decrements. The release makes the
+// task's plain stores visible at agent scope before any waiter can run.
+__device__ __forceinline__ void dag_put(DagWave &w, uint32_t p, unsigned long long datum) {
+    release_agent();
+    dag_put_one(w, p, datum);
+}
+
+// Several puts of one task behind a single release (a tile that satisfies
+// its right-column, bottom-row and corner promises at once).
+template <int N>
+__device__ __forceinline__ void dag_put_n(DagWave &w, const uint32_t (&p)[N], const unsigned long long (&datum)[N]) {
+    release_agent();
+#pragma unroll
+    for (int i = 0; i < N; ++i) dag_put_one(w, p[i], datum[i]);
 }
 
 // Kind concept:
