@@ -69,12 +69,12 @@ def wide_tree(H, rank, world, be, steps=2, split=7):
             "scaling": "strong", "bit_exact": True}
 
 
-def measure_triad(H, reps=20):
+def measure_triad(H, reps=20, n=1 << 28, sync=None):
     """forasync triad (BASELINE config 1): 2^28 fp32, a = b + 3*c; HIP events
-    on the stream the kernel is launched on; checked bit-exact."""
+    on the stream the kernel is launched on; checked bit-exact. `sync` (the
+    ranks' barrier) runs just before the timed launches when sharded."""
     import torch
 
-    n = 1 << 28
     g = torch.Generator(device="cuda").manual_seed(1)
     # one allocation, the three arrays staggered by 2 MiB + 4 KiB (the
     # STREAM-style array offset: HBM channels are not all hit at the same
@@ -92,6 +92,9 @@ def measure_triad(H, reps=20):
         H.triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), 3.0, n, st.cuda_stream)
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    if sync:
+        sync()
     e0.record(st)
     for _ in range(reps):
         H.triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), 3.0, n, st.cuda_stream)
@@ -203,6 +206,17 @@ def main():
         raise SystemExit(f"T3L mismatch: {tot} != {T3L_GOLD}")
     value = T3L_GOLD[0] * args.steps / elapsed
     wide = None if args.no_extras else wide_tree(H, rank, world, be)
+    shard_tri = None
+    if world > 1 and not args.no_extras:
+        # the 2^28 triad block-sharded over the ranks (no
+        # exchange); whole-job GB/s over the slowest rank's launch time
+        n_local = (1 << 28) // world
+        tr = measure_triad(H, n=n_local, sync=lambda: dist.barrier(world, be))
+        ms = dist.max_over_ranks(tr["ms"], world, be)
+        ok = dist.max_over_ranks(0.0 if tr["bit_exact"] else 1.0, world, be) == 0.0
+        shard_tri = {"workload": f"hclib_forasync 1-D triad, 2^28 fp32 block-sharded over {world} GPU(s)",
+                     "GB_per_s": 12 * n_local * world / ms / 1e6, "ms": ms, "scaling": "strong",
+                     "bit_exact": ok}
     if rank != 0:
         dist.shutdown(world)
         return
@@ -230,6 +244,8 @@ def main():
     }
     if wide:
         out["wide_tree"] = wide
+    if shard_tri:
+        out["forasync_sharded"] = shard_tri
     if world == 1 and not args.no_extras:
         tri = measure_triad(H)
         traffic = load_pmc_traffic()
