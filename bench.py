@@ -164,6 +164,54 @@ def cpu_baseline(threads, min_seconds=10.0):
                       f"oracle/hclib_cpu.c, {threads} worker threads, {total_s:.2f} s of search time"}
 
 
+def cpu_configs(threads, s1, s2, gpu):
+    """The same CPU runtime (oracle/, "port") on the other BASELINE configs,
+    so each GPU figure has its host-CPU counterpart from the same box and
+    run: fib(30) async/finish, SW 64K tile DAG (promises/futures), forasync
+    triad on 2^26 fp32 (bounded: 768 MiB of host arrays). Best of 2 each."""
+    import ctypes as C
+
+    import numpy as np
+
+    from oracle import loader as L
+
+    lib = L.cpu_runtime()
+    out = {"cores": threads, "kind": "port"}
+    best = []
+    for _ in range(2):
+        sec = C.c_double()
+        assert lib.ohc_fib(threads, 30, 0, C.byref(sec)) == 832040
+        best.append(sec.value)
+    out["fib30"] = {"tasks_per_s": 2692537 / min(best), "s": min(best),
+                    "gpu_over_cpu": gpu["fib30_gpu"]["tasks_per_s"] / (2692537 / min(best))}
+    best = []
+    for _ in range(2):
+        sec = C.c_double()
+        sc = lib.ohc_sw(threads, s1, len(s1), s2, len(s2), 256, 256, C.byref(sec))
+        assert sc == 128772, sc
+        best.append(sec.value)
+    cells = 65536.0 * 65536.0
+    out["sw_64k"] = {"cells_per_s": cells / min(best), "s": min(best),
+                     "gpu_over_cpu": gpu["sw_64k"]["cells_per_s"] / (cells / min(best))}
+    n = 1 << 26
+    rng = np.random.default_rng(1)
+    b = rng.random(n, dtype=np.float32)
+    c = rng.random(n, dtype=np.float32)
+    a = np.empty(n, dtype=np.float32)
+    fp = C.POINTER(C.c_float)
+    best = []
+    for _ in range(2):
+        sec = C.c_double()
+        lib.ohc_triad(threads, a.ctypes.data_as(fp), b.ctypes.data_as(fp), c.ctypes.data_as(fp),
+                      C.c_float(3.0), n, -1, 0, C.byref(sec))
+        best.append(sec.value)
+    assert np.array_equal(a, b + np.float32(3.0) * c)
+    out["forasync_triad_2p26"] = {"GB_per_s": 12 * n / min(best) / 1e9, "s": min(best),
+                                  "gpu_over_cpu": gpu["forasync_triad_2p28"]["GB_per_s"] /
+                                  (12 * n / min(best) / 1e9)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -298,6 +346,7 @@ def main():
                                      os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))))
         threads = max(1, min(threads, 16, os.cpu_count() or 1))
         out["cpu_baseline"] = cpu_baseline(threads)
+        out["cpu_configs"] = cpu_configs(threads, s1, s2, out["configs"])
     print(json.dumps(out), flush=True)
     dist.shutdown(world)
 
