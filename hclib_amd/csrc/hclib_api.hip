@@ -82,7 +82,8 @@ struct Runtime {
     bool mem_builtins = false;
     // stats (HCLIB_STATS analogue, src/hclib-runtime.c:83-104)
     unsigned long long host_tasks = 0, device_tasks = 0, end_finishes = 0, forasyncs = 0;
-    unsigned long long device_items = 0;
+    unsigned long long spawned = 0, future_waits = 0, end_finishes_nb = 0, yields = 0, yield_iters = 0;
+    unsigned long long device_items = 0, device_batches = 0, device_chunks_pushed = 0, device_chunks_stolen = 0;
     double device_ms = 0;
 };
 
@@ -165,6 +166,16 @@ void ensure_gpu(const char *who) {
     }
 }
 
+// the megakernel's scheduler counters of the launch that just ended
+// (include/hclib_hip.h: [13] batches, [14] chunks pushed, [15] chunks stolen)
+void add_sched_counters(Runtime &R) {
+    uint64_t c[16];
+    hclib_hip_last_sched_counters(c);
+    R.device_batches += c[13];
+    R.device_chunks_pushed += c[14];
+    R.device_chunks_stolen += c[15];
+}
+
 // run one device task kind to completion and write its outputs back
 void run_device_task(hclib_task_t *t) {
     Runtime &R = rt();
@@ -182,6 +193,7 @@ void run_device_task(hclib_task_t *t) {
         check_hip(hclib_hip_fib(a->n, &v, &r), "hclib_hip_fib");
         a->res = (long)v;
         R.device_items += r.tasks;
+        add_sched_counters(R);
         R.device_ms += r.kernel_ms;
         break;
     }
@@ -203,6 +215,7 @@ void run_device_task(hclib_task_t *t) {
         a->leaves = r.leaves;
         a->max_depth = r.max_depth;
         R.device_items += r.nodes;
+        add_sched_counters(R);
         R.device_ms += r.kernel_ms;
         break;
     }
@@ -251,6 +264,7 @@ void spawn(generic_frame_ptr fp, void *arg, hclib_future_t **futures, int nfutur
     t->non_blocking = non_blocking;
     t->finish = R.current;
     check_in(t->finish);
+    R.spawned++;
     t->waiting_on_index = -1;
     for (int i = 0; i < nfutures && i < MAX_NUM_WAITS; ++i) t->waiting_on[i] = futures[i];
     if (nfutures > MAX_NUM_WAITS) {
@@ -369,8 +383,10 @@ void hclib_yield(hclib_locale_t *locale) {
     (void)locale;
     Runtime &R = rt();
     if (!R.launched) die("hclib_yield called outside hclib_launch");
+    R.yields++;
     while (!R.ready.empty()) {
         const int nb = R.ready.back()->non_blocking;
+        R.yield_iters++;
         run_one();
         if (!nb) break;
     }
@@ -428,6 +444,7 @@ void hclib_end_finish(void) {
 // src/hclib-runtime.c:1280-1313
 void hclib_end_finish_nonblocking_helper(hclib_promise_t *event) {
     Runtime &R = rt();
+    R.end_finishes_nb++;
     Finish *f = R.current;
     f->finish_dep = event;
     R.current = f->parent;
@@ -618,6 +635,7 @@ void hclib_promise_put(hclib_promise_t *p, void *datum) {
 
 // hclib_future_wait, src/hclib-runtime.c:983-1025 (help while waiting)
 void *hclib_future_wait(hclib_future_t *f) {
+    rt().future_waits++;
     while (!f->owner->satisfied) {
         if (!run_one()) die("future_wait: the future can never be satisfied (deadlock)");
     }
@@ -909,12 +927,29 @@ void hclib_hip_register_forasync_body(void *fct, int body) {
 
 // hclib_print_runtime_stats, src/hclib-runtime.c:1370-1410
 void hclib_print_runtime_stats(FILE *fp) {
+    // the layout of the reference's HCLIB_STATS report (src/hclib-runtime.c:
+    // 1370-1410): one line per worker, then the totals. Worker 0 is the host
+    // control thread; the device's waves are reported as one line of their
+    // batches and chunk deque traffic (steals = chunks taken from a deque
+    // other than the wave's home deque).
     Runtime &R = rt();
+    fprintf(fp, "===== HClib statistics: =====\n");
     fprintf(fp,
-            "HCLIB STATS: host_tasks=%llu device_tasks=%llu device_items=%llu "
-            "device_ms=%.3f end_finishes=%llu forasyncs=%llu device_workers=%d\n",
-            R.host_tasks, R.device_tasks, R.device_items, R.device_ms, R.end_finishes,
-            R.forasyncs, hclib_hip_num_workers());
+            "  Worker 0: %llu tasks executed, %llu tasks spawned, %llu tasks scheduled, 0 steals, "
+            "0 stolen tasks, 0.000000 tasks per steal, stolen from = [ 0 ]\n",
+            R.host_tasks + R.device_tasks, R.spawned, R.spawned);
+    if (R.device_tasks)
+        fprintf(fp,
+                "  Device (%d waves): %llu device items executed in %llu batches, %llu chunks pushed, "
+                "%llu chunks stolen, %f items per batch, %.3f ms\n",
+                hclib_hip_num_workers(), R.device_items, R.device_batches, R.device_chunks_pushed,
+                R.device_chunks_stolen,
+                R.device_batches ? (double)R.device_items / (double)R.device_batches : 0.0, R.device_ms);
+    fprintf(fp,
+            "Total: %llu tasks, %llu end finishes, %llu future waits, %llu non-blocking end finishes, "
+            "0 ctx creates, %llu yields, %f iters per yield on average\n",
+            R.host_tasks + R.device_tasks + R.device_items, R.end_finishes, R.future_waits, R.end_finishes_nb,
+            R.yields, R.yields ? (double)R.yield_iters / (double)R.yields : 0.0);
 }
 
 }  // extern "C"

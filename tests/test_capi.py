@@ -95,3 +95,14 @@ def test_uts_c_program_on_gpu(golden, name):
     want = (f"Tree size = {g['nodes']}, tree depth = {g['depth']}, "
             f"num leaves = {g['leaves']}")
     assert want in r.stdout, r.stdout
+
+
+def test_hclib_stats_report_layout():
+    """HCLIB_STATS=1 prints the reference's report layout at finalize
+    (src/hclib-runtime.c:1370-1410): the banner, a per-worker line, totals."""
+    r = _run(_build("promise_chain"), env={"HCLIB_STATS": "1"})
+    assert r.returncode == 0, r.stderr
+    out = r.stdout
+    assert "===== HClib statistics: =====" in out
+    assert "  Worker 0: " in out and " tasks executed, " in out
+    assert "Total: " in out and " end finishes, " in out and " future waits, " in out
