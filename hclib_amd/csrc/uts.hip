@@ -536,7 +536,9 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
-    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", 8);
+    // hunger read every 32 batches, every 8 while many waves are hungry
+    // (scripts/sweep_uts.py: T1 1.37 -> 1.07 ms, T1XL 101 -> 97 ms, T3L even)
+    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", 32);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 1);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));

@@ -561,7 +561,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             if (hunger_in == 0) {
                 outst_cur = lane0(outst_pf);
                 if (lane == 0) outst_pf = ld_agent(&g->outstanding);
-                hunger_in = cfg.hunger;
+                // many hungry waves (ramp-up, a narrowing tree): read again
+                // soon; otherwise every cfg.hunger batches
+                const uint32_t hg = cfg.nwaves > outst_cur ? cfg.nwaves - outst_cur : 0u;
+                hunger_in = hg * 8u > cfg.nwaves ? (cfg.hunger + 3u) / 4u : cfg.hunger;
             }
             --hunger_in;
             outst = outst_cur;
@@ -664,6 +667,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         }
         // a push that would come near live items first moves the oldest
         // items out as chunks (rare: only bursts of wide nodes)
+        unsigned long long full_since = 0;
         while ((top - bot) + tout > kRoom) {
             uint32_t n = top - bot;
             if (n > pool.chunk) n = pool.chunk;
@@ -671,8 +675,18 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             for (uint32_t a = 0; a < pool.nq && !ok; ++a)
                 ok = enqueue_chunk<Kind, CAP>(pool, g, (home + a) % pool.nq, st, bot, n);
             if (!ok) {
-                if (lane == 0) dev_error(&g->err, kErrStackOverflow);
-                break;
+                // every deque is at its half-capacity mark: other waves are
+                // draining them, so wait (bounded) rather than fail at once
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                if (full_since == 0) full_since = now;
+                uint32_t e = 0;
+                if (lane == 0) e = ld_agent(&g->err);
+                if (lane0(e) || now - full_since > 100000ull * cfg.spin_limit) {
+                    if (lane == 0) dev_error(&g->err, kErrStackOverflow);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+                continue;
             }
             ++npush;
             bot += n;
