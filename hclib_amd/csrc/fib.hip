@@ -152,7 +152,8 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
                                                     : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);
     SchedConfig cfg;
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_HI", 256);
-    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", 2);
+    // scripts/sweep_uts.py fib30 (profiles/r01_s5/knob_sweeps.log): 32 -> 1.50 ms, 2 -> 1.70 ms
+    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", 32);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
