@@ -92,7 +92,7 @@ extern "C" int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t
             datum[p] = preput_datum ? preput_datum[p] : 0;
         }
     // one arena: ctl lines (head, tail, err), stats, then the arrays
-    const size_t o_ctl = 0, o_stats = 768, o_deps = 1024;
+    const size_t o_ctl = 0, o_stats = 1024, o_deps = 1280;
     const size_t o_woff = o_deps + up256((size_t)ntasks * 4 + 4);
     const size_t o_wait = o_woff + up256(woff.size() * 4);
     const size_t o_datum = o_wait + up256(waiters.size() * 4);

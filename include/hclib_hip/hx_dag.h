@@ -32,6 +32,7 @@
 namespace hx {
 
 constexpr uint32_t kDagEmpty = 0xffffffffu;
+constexpr uint32_t kDagSkip = 0xfffffffeu;  // a ready-list slot whose task its releaser ran
 
 enum : uint32_t { kErrDoublePut = 7 };
 
@@ -55,6 +56,9 @@ struct DagView {
 struct DagWave {
     DagView v;
     unsigned long long puts, releases;
+    uint32_t next;      // a task this wave's puts released and kept for itself
+    uint32_t skip_pos;  // (lane skip_lane) the ready-list slot that task gave up
+    int skip_lane;
 };
 
 // hclib_future_get on the device: the datum of a satisfied promise (one the
@@ -88,9 +92,32 @@ __device__ __forceinline__ void dag_put_one(DagWave &w, uint32_t p, unsigned lon
         return;
     }
     uint32_t rel = 0;
-    for (uint32_t k = b + (uint32_t)lane; k < e; k += 64) {
-        const uint32_t t = v.waiters[k];
-        if (add_agent(&v.deps[t], (uint32_t)-1) == 1u) {
+    for (uint32_t k0 = b; k0 < e; k0 += 64) {
+        const uint32_t k = k0 + (uint32_t)lane;
+        uint32_t t = kDagEmpty;
+        if (k < e) {
+            const uint32_t c = v.waiters[k];
+            if (add_agent(&v.deps[c], (uint32_t)-1) == 1u) t = c;
+        }
+        // the putter keeps one released task and runs it next, as the
+        // reference's put pushes waiters onto the putting worker's own deque
+        // and that worker pops it first (src/hclib-promise.c:224-240,
+        // src/hclib-runtime.c:488-530); the others go to the ready list
+        const unsigned long long m = __ballot(t != kDagEmpty);
+        if (m && w.next == kDagEmpty) {
+            const int leader = __builtin_ctzll(m);
+            w.next = (uint32_t)__builtin_amdgcn_readlane((int)t, leader);
+            w.skip_lane = leader;
+            if (lane == leader) {
+                // the task still owns one ready-list slot (the ticket count
+                // stays exact); it is marked skipped once the kept task runs,
+                // so this atomic's latency hides behind that task
+                w.skip_pos = add_agent(v.tail, 1u);
+                t = kDagEmpty;
+                ++rel;
+            }
+        }
+        if (t != kDagEmpty) {
             const uint32_t pos = add_agent(v.tail, 1u);
             st_agent(&v.ready[pos], t);
             ++rel;
@@ -123,36 +150,55 @@ __device__ __forceinline__ void dag_put_n(DagWave &w, const uint32_t (&p)[N], co
 //                              const uint32_t *payload);
 //        a wave-wide body: every lane enters; dag_get reads the futures it
 //        awaited, dag_put satisfies promises (wave-uniform calls).
+//
+// A wave runs the task its own puts kept (w.next) before taking a ticket;
+// that task's ready-list slot is then marked kDagSkip, and the wave whose
+// ticket lands on it takes another ticket. Every slot below ntasks is thus
+// filled exactly once, and a wave leaves on a ticket >= ntasks.
 template <class Kind>
 __device__ void run_dag_worker(const typename Kind::Ctx &ctx, const DagView &view) {
-    DagWave w{view, 0, 0};
+    DagWave w{view, 0, 0, kDagEmpty, 0, 0};
     const int lane = lane_id();
     unsigned long long ran = 0;
     while (true) {
-        uint32_t ticket = 0;
-        if (lane == 0) ticket = add_agent(view.head, 1u);
-        ticket = (uint32_t)__shfl((int)ticket, 0, 64);
-        if (ticket >= view.ntasks) break;
         uint32_t t = kDagEmpty;
-        if (lane == 0) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while ((t = ld_agent(&view.ready[ticket])) == kDagEmpty) {
-                if (ld_agent(view.err)) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * view.spin_ms) {
-                    dev_error(view.err, kErrSpinTimeout);
-                    break;
+        bool kept = false;
+        uint32_t pend_pos = 0;
+        int pend_lane = 0;
+        if (w.next != kDagEmpty) {
+            t = w.next;
+            w.next = kDagEmpty;
+            kept = true;
+            pend_pos = w.skip_pos;
+            pend_lane = w.skip_lane;
+        } else {
+            uint32_t ticket = 0;
+            if (lane == 0) ticket = add_agent(view.head, 1u);
+            ticket = (uint32_t)__shfl((int)ticket, 0, 64);
+            if (ticket >= view.ntasks) break;
+            if (lane == 0) {
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                while ((t = ld_agent(&view.ready[ticket])) == kDagEmpty) {
+                    if (ld_agent(view.err)) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * view.spin_ms) {
+                        dev_error(view.err, kErrSpinTimeout);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                __builtin_amdgcn_s_sleep(1);
             }
+            t = (uint32_t)__shfl((int)t, 0, 64);
+            if (t == kDagSkip) continue;
+            if (t == kDagEmpty) break;
         }
-        t = (uint32_t)__shfl((int)t, 0, 64);
-        if (t == kDagEmpty || t >= view.ntasks) {
-            if (t != kDagEmpty && lane == 0) dev_error(view.err, kErrBadTask);
+        if (t >= view.ntasks) {
+            if (lane == 0) dev_error(view.err, kErrBadTask);
             break;
         }
         acquire_agent();
         Kind::run(ctx, w, t, view.payload + (size_t)t * view.payload_words);
         ++ran;
+        if (kept && lane == pend_lane) st_agent(&view.ready[pend_pos], kDagSkip);
     }
     if (lane == 0) {
         add_agent(&view.stats[0], ran);
