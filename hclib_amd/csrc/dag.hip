@@ -49,8 +49,6 @@ extern "C" int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t
         set_error("hclib_hip_dag_begin: a DAG launch is already open (call hclib_hip_dag_end)");
         return HCLIB_HIP_EINVAL;
     }
-    HX_TRY(ensure_device());
-    Module &m = mod();
     const uint32_t nawaits = ntasks ? await_off[ntasks] : 0;
     if (nawaits && !await_ids) {
         set_error("hclib_hip_dag_begin: await_ids is NULL");
@@ -91,6 +89,9 @@ extern "C" int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t
             sat[p] = 1;
             datum[p] = preput_datum ? preput_datum[p] : 0;
         }
+    // the graph is valid: from here on a device is needed
+    HX_TRY(ensure_device());
+    Module &m = mod();
     // one arena: ctl lines (head, tail, err), stats, then the arrays
     const size_t o_ctl = 0, o_stats = 1024, o_deps = 1280;
     const size_t o_woff = o_deps + up256((size_t)ntasks * 4 + 4);

@@ -109,3 +109,32 @@ def test_atomic_calibrate_rejects_bad_arguments():
         H.atomic_calibrate(3, 16)
     with pytest.raises(H.HclibError):
         H.atomic_calibrate(H.ATOMIC_HOT_WORD, 1)
+
+
+def test_dag_begin_checks_arguments_then_needs_a_gpu():
+    """hclib_hip_dag_begin validates the graph on the host (out-of-range
+    promise ids, non-monotone CSR) before touching a device, and without a
+    gfx950 device a valid graph fails with ENODEV — no CPU fallback."""
+    import ctypes as C
+
+    import torch
+
+    lib = C.CDLL(H.LIB_PATH)
+    out = (C.c_char * 64)()
+    off = (C.c_uint32 * 3)(0, 1, 2)
+    bad_ids = (C.c_uint32 * 2)(0, 7)  # promise 7 of 2
+    fn = lib.hclib_hip_dag_begin
+    fn.restype = C.c_int
+    rc = fn(C.c_uint32(2), C.c_uint32(2), C.c_uint32(0), None, off, bad_ids, None, None, 4,
+            C.c_uint32(100), C.byref(out))
+    assert rc == -2  # EINVAL, with or without a GPU
+    nonmono = (C.c_uint32 * 3)(0, 2, 1)
+    ids = (C.c_uint32 * 2)(0, 1)
+    rc = fn(C.c_uint32(2), C.c_uint32(2), C.c_uint32(0), None, nonmono, ids, None, None, 4,
+            C.c_uint32(100), C.byref(out))
+    assert rc == -2
+    if torch.cuda.is_available():
+        return
+    rc = fn(C.c_uint32(2), C.c_uint32(2), C.c_uint32(0), None, off, ids, None, None, 4,
+            C.c_uint32(100), C.byref(out))
+    assert rc == -1  # ENODEV: a valid graph needs the GPU
