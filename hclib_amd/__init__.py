@@ -80,6 +80,7 @@ EXPORTS_HIP = [
     "hclib_hip_version", "hclib_hip_forasync", "hclib_hip_forasync_triad_f32",
     "hclib_hip_num_workers", "hclib_hip_uts_search", "hclib_hip_uts_num_children_host",
     "hclib_hip_fib", "hclib_hip_sw", "hclib_hip_last_sched_counters",
+    "hclib_hip_sw_band_begin", "hclib_hip_sw_band_rows", "hclib_hip_sw_band_end",
 ]
 
 _lib = None
@@ -109,6 +110,13 @@ def lib():
         L.hclib_hip_fib.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(FibResult)]
         L.hclib_hip_sw.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_int,
                                    C.c_int, C.POINTER(C.c_int), C.POINTER(SwResult)]
+        L.hclib_hip_sw_band_begin.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+                                              C.c_int, C.c_int, C.c_int, C.c_int,
+                                              C.POINTER(C.c_void_p)]
+        L.hclib_hip_sw_band_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                             C.c_void_p]
+        L.hclib_hip_sw_band_end.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int),
+                                            C.POINTER(C.c_uint64)]
         L.hclib_hip_atomic_calibrate.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double),
                                                  C.POINTER(C.c_double)]
         _lib = L
@@ -214,6 +222,34 @@ def sw(s1: bytes, s2: bytes, tile_w: int, tile_h: int):
     _check(lib().hclib_hip_sw(s1, len(s1), s2, len(s2), tile_w, tile_h, C.byref(score),
                               C.byref(r)), "hclib_hip_sw")
     return score.value, {k: getattr(r, k) for k, _ in SwResult._fields_}
+
+
+class SwBand:
+    """One rank's band of tile columns [j0, j1) of the SW tile grid
+    (hclib_hip_sw_band_*, include/hclib_hip.h). rows() launches tile rows
+    [i0, i1) on `stream` (a raw hipStream_t handle, e.g. torch's
+    current_stream().cuda_stream); left_in / right_out are device pointers
+    to nth*th int32 (H of matrix columns j0*tw and j1*tw, rows 1..)."""
+
+    def __init__(self, s1: bytes, s2: bytes, tile_w: int, tile_h: int, j0: int, j1: int):
+        self.ntw, self.nth = len(s1) // tile_w, len(s2) // tile_h
+        self.tile_w, self.tile_h, self.j0, self.j1 = tile_w, tile_h, j0, j1
+        h = C.c_void_p()
+        _check(lib().hclib_hip_sw_band_begin(s1, len(s1), s2, len(s2), tile_w, tile_h, j0, j1,
+                                             C.byref(h)), "hclib_hip_sw_band_begin")
+        self._h = h
+
+    def rows(self, i0: int, i1: int, left_in: int | None, right_out: int | None, stream: int):
+        _check(lib().hclib_hip_sw_band_rows(self._h, i0, i1, left_in, right_out, stream),
+               "hclib_hip_sw_band_rows")
+
+    def end(self, stream: int):
+        """Synchronise, free; returns (bottom-right cell of the band, tiles run)."""
+        corner, tiles = C.c_int(), C.c_uint64()
+        h, self._h = self._h, None
+        _check(lib().hclib_hip_sw_band_end(h, stream, C.byref(corner), C.byref(tiles)),
+               "hclib_hip_sw_band_end")
+        return corner.value, tiles.value
 
 
 def sw_map(text: bytes) -> bytes:

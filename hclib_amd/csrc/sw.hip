@@ -48,6 +48,14 @@ struct SwCtx {
     // row-pipelined schedule: a tile's bottom row is published as 8-byte
     // {tag = 1, H} granules — the data is the promise (R2 hand-off)
     unsigned long long *gbot;  // [tiles][tw]
+    // column band (multi-GPU sharding by tile columns; the whole grid is
+    // j0 = 0, j1 = ntw, i0 = 0, i1 = nth): tile columns [j0, j1), tile rows
+    // [i0, i1) of this launch. left_in = H of matrix column j0*tw, rows
+    // 1..nth*th (the left band's right column; null when j0 == 0);
+    // right_out receives H of matrix column j1*tw (null: not wanted)
+    int j0, j1, i0, i1;
+    const int *left_in;  // [nth*th]
+    int *right_out;      // [nth*th]
 };
 
 // alignment_score_matrix (smith_waterman.cpp:36-43) row for s2 code a, plus
@@ -446,9 +454,16 @@ __global__ __launch_bounds__(64) void k_sw_rows(SwCtx c) {
     unsigned long long ntile = 0, cyc_tile = 0, cyc_wait = 0;
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
     bool ok = true;
-    for (int i = blockIdx.x; i < c.nth && ok; i += gridDim.x) {
-        int corner = (i == 0) ? 0 : -(i * c.th);  // H(R0-1, C0-1) of tile (i, 0): boundary column
-        for (int j = 0; j < c.ntw && ok; ++j) {
+    for (int i = c.i0 + (int)blockIdx.x; i < c.i1 && ok; i += gridDim.x) {
+        // H(R0-1, C0-1) of tile (i, j0): the boundary column, or for a band
+        // the left band's right column one row above the tile
+        int corner = (i == 0) ? -(c.j0 * c.tw) : -(i * c.th);
+        if (c.j0 > 0) {
+            if (i > 0) corner = ld_agent(&c.left_in[(size_t)i * c.th - 1]);
+            for (int r = lane; r < c.th; r += 64) lds_left[r] = ld_agent(&c.left_in[(size_t)i * c.th + r]);
+            __syncthreads();
+        }
+        for (int j = c.j0; j < c.j1 && ok; ++j) {
             const uint32_t t = (uint32_t)(i * c.ntw + j);
             const unsigned long long t0 = __builtin_amdgcn_s_memtime();
             ok = sw_tile<true>(c, t, lds_top, lds_bot, lds_s1, lds_left, lds_right, corner, ph);
@@ -459,6 +474,9 @@ __global__ __launch_bounds__(64) void k_sw_rows(SwCtx c) {
             cyc_tile += __builtin_amdgcn_s_memtime() - t0;
             ++ntile;
         }
+        // the band's right column (now in lds_left) goes to the right band
+        if (ok && c.right_out)
+            for (int r = lane; r < c.th; r += 64) c.right_out[(size_t)i * c.th + r] = lds_left[r];
     }
     if (lane == 0) {
         add_agent(&c.stats[0], ntile);
@@ -567,6 +585,12 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     c.ntw = (int)ntw;
     c.nth = (int)nth;
     c.spin_ms = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
+    c.j0 = 0;
+    c.j1 = (int)ntw;
+    c.i0 = 0;
+    c.i1 = (int)nth;
+    c.left_in = nullptr;
+    c.right_out = nullptr;
     int rc = HCLIB_HIP_OK;
     auto fail = [&](int r) { (void)hipFree(d); return r; };
     if ((rc = hip_check(hipMemcpyAsync((void *)c.s1, s1, b_s1, hipMemcpyHostToDevice, m.stream), "copy s1"))) return fail(rc);
@@ -663,5 +687,134 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         result->tile_us = st[0] ? (double)st[2] / st[0] / 2400.0 : 0.0;
         result->release_us = st[0] ? (double)st[3] / st[0] / 2400.0 : 0.0;
     }
+    return HCLIB_HIP_OK;
+}
+
+// ------------------------------------------------- column-band sessions
+// Multi-GPU SW: each rank owns a band of tile columns
+// and runs the row schedule over it in blocks of tile rows; between blocks
+// the host moves the band's right column to the next rank (RCCL send/recv on
+// the same stream, hclib_amd/dist.py). The band keeps its granules, s1 and s2
+// on the device across blocks, so a block only needs its left column.
+struct hclib_hip_sw_band {
+    SwCtx c;
+    char *mem;
+    size_t lds;
+    int grid_cap;
+};
+
+extern "C" int hclib_hip_sw_band_begin(const int8_t *s1, size_t n1, const int8_t *s2, size_t n2, int tw, int th,
+                                       int j0, int j1, hclib_hip_sw_band_t **out) {
+    if (!out || !s1 || !s2 || tw < 1 || th < 1 || tw > 16384) {
+        set_error("hclib_hip_sw_band_begin: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    *out = nullptr;
+    const size_t ntw = n1 / (size_t)tw, nth = n2 / (size_t)th;
+    if (ntw == 0 || nth == 0 || ntw * nth > 0x7fffffffull || j0 < 0 || j1 <= j0 || (size_t)j1 > ntw) {
+        set_error("hclib_hip_sw_band_begin: empty grid or band [%d, %d) outside 0..%zu", j0, j1, ntw);
+        return HCLIB_HIP_EINVAL;
+    }
+    for (size_t k = 0; k < ntw * (size_t)tw; ++k)
+        if (s1[k] < 1 || s1[k] > 4) { set_error("hclib_hip_sw_band_begin: s1 must be coded 1..4"); return HCLIB_HIP_EINVAL; }
+    for (size_t k = 0; k < nth * (size_t)th; ++k)
+        if (s2[k] < 1 || s2[k] > 4) { set_error("hclib_hip_sw_band_begin: s2 must be coded 1..4"); return HCLIB_HIP_EINVAL; }
+    const size_t lds = 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + 68 * 4 + 2 * (size_t)((tw + 3) & ~3) + 16 +
+                       2 * (size_t)(((th + 3) & ~3) * 4);
+    if (lds > 64 * 1024) {
+        set_error("hclib_hip_sw_band_begin: tile too large for the row schedule");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    Module &m = mod();
+    const size_t nt = ntw * nth, b_s1 = ntw * tw, b_s2 = nth * th, b_gbot = nt * tw * 8;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t total = al(b_s1) + al(b_s2) + al(b_gbot) + 1024;
+    hclib_hip_sw_band *h = new hclib_hip_sw_band();
+    if (hipMalloc((void **)&h->mem, total) != hipSuccess) {
+        delete h;
+        set_error("hclib_hip_sw_band_begin: hipMalloc(%zu) failed", total);
+        return HCLIB_HIP_ENOMEM;
+    }
+    SwCtx &c = h->c;
+    memset(&c, 0, sizeof(c));
+    size_t off = 0;
+    c.s1 = (const int8_t *)(h->mem + off); off += al(b_s1);
+    c.s2 = (const int8_t *)(h->mem + off); off += al(b_s2);
+    c.gbot = (unsigned long long *)(h->mem + off); off += al(b_gbot);
+    uint32_t *misc = (uint32_t *)(h->mem + off);
+    c.err = misc + 128;
+    c.stats = (unsigned long long *)(misc + 192);
+    c.tw = tw;
+    c.th = th;
+    c.ntw = (int)ntw;
+    c.nth = (int)nth;
+    c.j0 = j0;
+    c.j1 = j1;
+    c.spin_ms = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
+    h->lds = lds;
+    h->grid_cap = m.num_cus;
+    int rc;
+    if ((rc = hip_check(hipMemcpy((void *)c.s1, s1, b_s1, hipMemcpyHostToDevice), "copy s1")) ||
+        (rc = hip_check(hipMemcpy((void *)c.s2, s2, b_s2, hipMemcpyHostToDevice), "copy s2")) ||
+        (rc = hip_check(hipMemset(misc, 0, 1024), "memset")) ||
+        (rc = hip_check(hipMemset(c.gbot, 0, b_gbot), "memset granules"))) {
+        (void)hipFree(h->mem);
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_sw_band_rows(hclib_hip_sw_band_t *h, int i0, int i1, const int *left_in, int *right_out,
+                                      void *stream) {
+    if (!h || i0 < 0 || i1 <= i0 || i1 > h->c.nth || (h->c.j0 > 0 && !left_in)) {
+        set_error("hclib_hip_sw_band_rows: invalid arguments (rows [%d, %d), left column %s)", i0, i1,
+                  left_in ? "given" : "missing");
+        return HCLIB_HIP_EINVAL;
+    }
+    SwCtx c = h->c;
+    c.i0 = i0;
+    c.i1 = i1;
+    c.left_in = left_in;
+    c.right_out = right_out;
+    // one wave owns each tile row; every wave of the block is resident, so
+    // each granule wait ends (rows above i0 finished in an earlier launch)
+    int grid = i1 - i0;
+    if (grid > h->grid_cap) grid = h->grid_cap;
+    hipLaunchKernelGGL(k_sw_rows, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
+    return hip_check(hipGetLastError(), "k_sw_rows (band) launch");
+}
+
+extern "C" int hclib_hip_sw_band_end(hclib_hip_sw_band_t *h, void *stream, int *corner, uint64_t *tiles) {
+    if (!h) {
+        set_error("hclib_hip_sw_band_end: null band");
+        return HCLIB_HIP_EINVAL;
+    }
+    int rc = hip_check(hipStreamSynchronize((hipStream_t)stream), "k_sw_rows (band)");
+    uint32_t herr = 0;
+    unsigned long long st[4] = {0}, g = 0;
+    const SwCtx &c = h->c;
+    if (!rc) {
+        (void)hipMemcpy(&herr, c.err, 4, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(st, c.stats, sizeof(st), hipMemcpyDeviceToHost);
+        // bottom-right cell of the band's last tile (the score for the last band)
+        const size_t t = (size_t)(c.nth - 1) * c.ntw + (c.j1 - 1);
+        (void)hipMemcpy(&g, c.gbot + t * c.tw + (c.tw - 1), 8, hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(h->mem);
+    delete h;
+    if (rc) return rc;
+    if (herr) {
+        set_error("hclib_hip_sw_band_end: device error %u", herr);
+        return HCLIB_HIP_EDEVICE;
+    }
+    if ((g >> 32) != 1ull) {
+        set_error("hclib_hip_sw_band_end: the band's last tile was never computed (rows missing)");
+        return HCLIB_HIP_EDEVICE;
+    }
+    if (corner) *corner = (int)(uint32_t)g;
+    if (tiles) *tiles = st[0];
     return HCLIB_HIP_OK;
 }

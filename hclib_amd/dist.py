@@ -93,3 +93,127 @@ def shutdown(world: int) -> None:
         import torch.distributed as dist
 
         dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ SW bands
+# Smith-Waterman sharded by tile columns. Rank r owns
+# the contiguous band of tile columns sw_bands(ntw, world)[r] and runs it in
+# blocks of tile rows (sw_blocks). Its only input from another rank is the
+# left band's right column (the reference's right_column promises of tile
+# column j0-1 and their bottom-right corners, smith_waterman.cpp:212-226),
+# which arrives per block as one point-to-point message; it sends its own
+# right column on to rank r+1 the same way. Block b of rank r therefore
+# overlaps block b+1 of rank r-1 (a software pipeline over the ranks). Over
+# RCCL every step is stream-ordered (recv -> kernel -> send on the device,
+# the host never waits); over gloo (CPU tests, shared-device rehearsals) the
+# messages are staged through host memory.
+
+
+def sw_bands(ntw: int, world: int):
+    """Contiguous tile-column bands [(j0, j1)] for each rank (ntw >= world)."""
+    if ntw < world:
+        raise ValueError(f"{ntw} tile columns cannot be split over {world} ranks")
+    return [(r * ntw // world, (r + 1) * ntw // world) for r in range(world)]
+
+
+def sw_blocks(nth: int, block_rows: int):
+    """Tile-row blocks [(i0, i1)] exchanged as one message each."""
+    if block_rows < 1:
+        raise ValueError("block_rows must be >= 1")
+    return [(i, min(nth, i + block_rows)) for i in range(0, nth, block_rows)]
+
+
+def sw_block_rows(ntw: int, nth: int, world: int) -> int:
+    """Rows per exchanged block. With band width W = ntw/world tiles, a block
+    of K tile rows has a span of K + W - 1 tiles and the pipeline runs
+    nth/K + world - 1 block steps, so the span is minimised near
+    K = sqrt((W - 1) * nth / (world - 1))."""
+    if world <= 1:
+        return nth
+    w = max(1, ntw // world)
+    k = int(round(((w - 1) * nth / (world - 1)) ** 0.5))
+    return max(1, min(nth, k))
+
+
+class _HipBand:
+    """A band on the GPU through hclib_hip_sw_band_* (the C-ABI)."""
+
+    def __init__(self, s1, s2, tw, th, j0, j1):
+        import torch
+
+        from . import SwBand
+
+        self.band = SwBand(s1, s2, tw, th, j0, j1)
+        self.stream = torch.cuda.current_stream().cuda_stream
+
+    def rows(self, i0, i1, left, right):
+        self.band.rows(i0, i1, None if left is None else left.data_ptr(),
+                       None if right is None else right.data_ptr(), self.stream)
+
+    def end(self):
+        return self.band.end(self.stream)
+
+
+class ShardedSw:
+    """One rank's share of a sharded SW run. __init__ uploads the band
+    (outside any timed region); run() executes the pipeline once and
+    returns (score, tiles over all ranks). `band_factory(s1, s2, tw, th, j0,
+    j1)` defaults to the HIP band; the CPU tests pass a host DP band."""
+
+    def __init__(self, s1: bytes, s2: bytes, tw: int, th: int, rank: int, world: int,
+                 backend: str = "nccl", block_rows: int = 16, band_factory=None, device=None):
+        import torch
+
+        self.rank, self.world, self.backend = rank, world, backend
+        self.th = th
+        ntw, nth = len(s1) // tw, len(s2) // th
+        self.j0, self.j1 = sw_bands(ntw, world)[rank]
+        self.blocks = sw_blocks(nth, block_rows)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        n = nth * th
+        self.left = torch.empty(n, dtype=torch.int32, device=device) if rank > 0 else None
+        self.right = torch.empty(n, dtype=torch.int32, device=device) if rank < world - 1 else None
+        self.band = (band_factory or _HipBand)(s1, s2, tw, th, self.j0, self.j1)
+
+    def _recv(self, t):
+        import torch
+        import torch.distributed as dist
+
+        if self.backend == "nccl" or t.device.type == "cpu":
+            dist.recv(t, src=self.rank - 1)
+        else:  # gloo carries host tensors only
+            h = torch.empty_like(t, device="cpu")
+            dist.recv(h, src=self.rank - 1)
+            t.copy_(h)
+
+    def _send(self, t):
+        import torch.distributed as dist
+
+        if self.backend == "nccl" or t.device.type == "cpu":
+            dist.send(t, dst=self.rank + 1)
+        else:
+            dist.send(t.cpu(), dst=self.rank + 1)
+
+    def run(self):
+        import torch
+
+        th = self.th
+        for i0, i1 in self.blocks:
+            if self.left is not None:
+                self._recv(self.left[i0 * th:i1 * th])
+            self.band.rows(i0, i1, self.left, self.right)
+            if self.right is not None:
+                self._send(self.right[i0 * th:i1 * th])
+        corner, tiles = self.band.end()
+        if self.world == 1:
+            return corner, tiles
+        import torch.distributed as dist
+
+        dev = _device(self.backend)
+        sc = torch.tensor([corner if self.rank == self.world - 1 else 0], dtype=torch.int64, device=dev)
+        dist.broadcast(sc, src=self.world - 1)
+        tt = torch.tensor([tiles], dtype=torch.int64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        return int(sc[0]), int(tt[0])

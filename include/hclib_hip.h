@@ -282,6 +282,28 @@ typedef struct {
 int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_t n2, int tw, int th,
                  int *score, hclib_hip_sw_result_t *result);
 
+/* Column-band session (multi-GPU SW, one band of tile columns per rank).
+ * The reference runs the whole tile DAG in one address space
+ * (smith_waterman.cpp:168-235); sharded, rank r owns tile columns [j0, j1)
+ * and its only inputs from other ranks are the left band's right column
+ * (the reference's right_column promises of tile column j0-1, :212-216) and
+ * its bottom-right corners (:222-226), both carried by one int array:
+ *   begin   uploads s1/s2 (coded 1..4) and allocates the band's granules;
+ *   rows    launches tile rows [i0, i1) of the band on `stream` (a
+ *           hipStream_t); left_in = device array of nth*th ints holding H of
+ *           matrix column j0*tw for rows 1..nth*th (rows up to i1*th must be
+ *           in place; NULL only when j0 == 0); right_out (device, nth*th
+ *           ints, or NULL) receives H of column j1*tw for the same rows;
+ *   end     synchronises the stream, checks the device error word, writes
+ *           the band's bottom-right cell (the score for the last band) and
+ *           the tiles executed, and frees the band. */
+typedef struct hclib_hip_sw_band hclib_hip_sw_band_t;
+int hclib_hip_sw_band_begin(const int8_t *s1, size_t n1, const int8_t *s2, size_t n2, int tw, int th,
+                            int j0, int j1, hclib_hip_sw_band_t **band);
+int hclib_hip_sw_band_rows(hclib_hip_sw_band_t *band, int i0, int i1, const int *left_in, int *right_out,
+                           void *stream);
+int hclib_hip_sw_band_end(hclib_hip_sw_band_t *band, void *stream, int *corner, uint64_t *tiles);
+
 #ifdef __cplusplus
 }
 #endif

@@ -138,3 +138,25 @@ def test_dag_begin_checks_arguments_then_needs_a_gpu():
     rc = fn(C.c_uint32(2), C.c_uint32(2), C.c_uint32(0), None, off, ids, None, None, 4,
             C.c_uint32(100), C.byref(out))
     assert rc == -1  # ENODEV: a valid graph needs the GPU
+
+
+def test_sw_band_checks_arguments_then_needs_a_gpu():
+    """hclib_hip_sw_band_*: bands outside the tile grid, uncoded sequences and
+    a missing left column are rejected on the host; without a gfx950 device a
+    valid band fails with ENODEV — no CPU fallback."""
+    import torch
+
+    s = bytes([1, 2, 3, 4] * 64)
+    with pytest.raises(H.HclibError, match="outside"):
+        H.SwBand(s, s, 64, 64, 2, 5)  # 4 tile columns
+    with pytest.raises(H.HclibError, match="outside"):
+        H.SwBand(s, s, 64, 64, 1, 1)
+    with pytest.raises(H.HclibError, match="coded"):
+        H.SwBand(bytes(256), s, 64, 64, 0, 4)
+    with pytest.raises(H.HclibError, match="invalid"):
+        H._check(H.lib().hclib_hip_sw_band_rows(None, 0, 1, None, None, None), "rows")
+    with pytest.raises(H.HclibError, match="null"):
+        H._check(H.lib().hclib_hip_sw_band_end(None, None, None, None), "end")
+    if not torch.cuda.is_available():
+        with pytest.raises(H.HclibError):
+            H.SwBand(s, s, 64, 64, 1, 3)

@@ -52,3 +52,103 @@ def test_sharded_uts_counts_combine_over_gloo(golden, world):
     for r, tot, t in res:
         assert tot == (g["nodes"], g["leaves"], g["depth"])
         assert t == world - 1
+
+
+# ---------------------------------------------------------------- SW bands
+# The sharded Smith-Waterman pipeline (hclib_amd/dist.py ShardedSw) over
+# gloo: every rank runs its band of tile columns with a host DP standing in
+# for the HIP band kernel (tests/test_gpu.py runs the same pipeline on the
+# GPU), exchanging right columns block by block. Checked against the oracle:
+# the score, and each band's right column against the oracle's last column
+# of the matrix cut at that band's right edge (the column does not depend on
+# anything to its right).
+
+_M = [[-1] * 5, [-1, 2, -4, -2, -4], [-1, -4, 2, -4, -2], [-1, -2, -4, 2, -4], [-1, -4, -2, -4, 2]]
+
+
+class _HostBand:
+    """Host DP of one band: H[0][c] = -c, left column from the left band
+    (or -r), smith_waterman.cpp:201-210 recurrence."""
+
+    def __init__(self, s1, s2, tw, th, j0, j1):
+        self.s1, self.s2, self.th = s1, s2, th
+        self.c0, self.c1 = j0 * tw, j1 * tw
+        self.prev = [-c for c in range(self.c0, self.c1 + 1)]  # H[row][c0..c1]
+        self.row = 0
+        self.tiles = 0
+        self.tw_count = j1 - j0
+
+    def rows(self, i0, i1, left, right):
+        assert self.row == i0 * self.th
+        for r in range(i0 * self.th + 1, i1 * self.th + 1):
+            cur = [int(left[r - 1]) if left is not None else -r]
+            m = _M[self.s2[r - 1]]
+            for k, c in enumerate(range(self.c0 + 1, self.c1 + 1)):
+                cur.append(max(cur[k] - 1, self.prev[k + 1] - 1, self.prev[k] + m[self.s1[c - 1]]))
+            if right is not None:
+                right[r - 1] = cur[-1]
+            self.prev = cur
+        self.row = i1 * self.th
+        self.tiles += (i1 - i0) * self.tw_count
+
+    def end(self):
+        return self.prev[-1], self.tiles
+
+
+def _sw_worker(rank, world, port, s1, s2, tw, th, block_rows, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    import torch
+
+    from hclib_amd import dist
+
+    r, w, _ = dist.init_from_env("gloo")
+    job = dist.ShardedSw(s1, s2, tw, th, r, w, "gloo", block_rows, band_factory=_HostBand,
+                         device=torch.device("cpu"))
+    score, tiles = job.run()
+    right = None if job.right is None else job.right.tolist()
+    dist.barrier(w, "gloo")
+    dist.shutdown(w)
+    q.put((r, score, tiles, job.j1, right))
+
+
+@pytest.mark.parametrize("world,block_rows", [(2, 2), (3, 1), (3, 5)])
+def test_sharded_sw_pipeline_over_gloo(world, block_rows):
+    import random
+
+    from oracle import loader as L
+
+    rng = random.Random(world * 10 + block_rows)
+    tw, th = 8, 6
+    s1 = bytes(rng.randint(1, 4) for _ in range(7 * tw + 3))  # ragged tails are dropped
+    s2 = bytes(rng.randint(1, 4) for _ in range(5 * th + 2))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sw_worker, args=(r, world, port, s1, s2, tw, th, block_rows, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = L.sw_score(s1, s2, tw, th)
+    for r, score, tiles, j1, right in res:
+        assert score == want
+        assert tiles == 7 * 5
+        if right is not None:
+            _, _, col = L.sw_score(s1[:j1 * tw], s2, tw, th, want_edges=True)
+            assert right == col[1:]
+
+
+def test_sw_band_and_block_split():
+    from hclib_amd import dist
+
+    assert dist.sw_bands(256, 8) == [(32 * r, 32 * r + 32) for r in range(8)]
+    assert dist.sw_bands(7, 3) == [(0, 2), (2, 4), (4, 7)]
+    assert dist.sw_blocks(10, 4) == [(0, 4), (4, 8), (8, 10)]
+    with pytest.raises(ValueError):
+        dist.sw_bands(2, 3)
+    with pytest.raises(ValueError):
+        dist.sw_blocks(4, 0)

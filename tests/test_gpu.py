@@ -274,6 +274,101 @@ def test_sw_both_schedules(golden, sched, monkeypatch):
         assert score == L.sw_score(a, b, tw, th), (n1, n2, tw, th)
 
 
+def _sw_bands_in_order(s1, s2, tw, th, nbands, block_rows):
+    """Every band of an nbands-way column split, run one after the other on
+    cuda:0 through hclib_hip_sw_band_* in blocks of tile rows; band r's left
+    column is band r-1's right column (what ShardedSw moves between ranks)."""
+    import torch
+
+    from hclib_amd import dist
+
+    ntw, nth = len(s1) // tw, len(s2) // th
+    stream = torch.cuda.current_stream().cuda_stream
+    left, score, tiles, rights = None, None, 0, []
+    for r, (j0, j1) in enumerate(dist.sw_bands(ntw, nbands)):
+        band = H.SwBand(s1, s2, tw, th, j0, j1)
+        right = None
+        if r < nbands - 1:
+            right = torch.full((nth * th,), -(1 << 30), dtype=torch.int32, device="cuda")
+        for i0, i1 in dist.sw_blocks(nth, block_rows):
+            band.rows(i0, i1, None if left is None else left.data_ptr(),
+                      None if right is None else right.data_ptr(), stream)
+        score, t = band.end(stream)
+        tiles += t
+        rights.append((j1, None if right is None else right.cpu().tolist()))
+        left = right
+    return score, tiles, rights
+
+
+@pytest.mark.parametrize("n1,n2,tw,th,nbands,block_rows", [
+    (1000, 777, 64, 64, 3, 2), (2048, 1024, 256, 256, 4, 1), (700, 900, 64, 300, 2, 2),
+    (4096, 4096, 256, 512, 16, 3), (513, 1025, 17, 13, 5, 7)])
+def test_sw_column_bands_vs_oracle(n1, n2, tw, th, nbands, block_rows):
+    """Multi-GPU SW's band kernel: each band's right column is
+    the oracle's last column of the matrix cut at the band's edge, and the
+    last band's corner is the score; every tile runs once."""
+    rng = np.random.default_rng(n1 + n2 + nbands)
+    s1 = bytes(rng.integers(1, 5, n1, dtype=np.int8).tobytes())
+    s2 = bytes(rng.integers(1, 5, n2, dtype=np.int8).tobytes())
+    score, tiles, rights = _sw_bands_in_order(s1, s2, tw, th, nbands, block_rows)
+    assert score == L.sw_score(s1, s2, tw, th)
+    assert tiles == (n1 // tw) * (n2 // th)
+    for j1, right in rights:
+        if right is not None:
+            _, _, col = L.sw_score(s1[:j1 * tw], s2, tw, th, want_edges=True)
+            assert right == col[1:], j1
+
+
+def test_sw_64k_golden_in_column_bands(golden):
+    """The 64K config split into 8 column bands of 32 tile columns, 16 tile
+    rows per exchanged block (bench.py's N=8 shape): score 128772."""
+    s1, s2 = _sw_inputs("huge")
+    score, tiles, _ = _sw_bands_in_order(s1[:65536], s2[:65536], 256, 256, 8, 16)
+    assert score == golden("sw_goldens.json")["sw64k"]["score"] == 128772
+    assert tiles == 65536
+
+
+def _sw_rank(rank, world, port, s1, s2, tw, th, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    from hclib_amd import dist
+
+    r, w, _ = dist.init_from_env("gloo", share_device=True)
+    job = dist.ShardedSw(s1, s2, tw, th, r, w, "gloo", block_rows=4)
+    score, tiles = job.run()
+    dist.barrier(w, "gloo")
+    dist.shutdown(w)
+    q.put((r, score, tiles))
+
+
+def test_sharded_sw_two_ranks_sharing_the_gpu(golden):
+    """ShardedSw end to end with two processes (gloo, both on cuda:0): the
+    published 'large' score, every tile once over the ranks."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    g = golden("sw_goldens.json")["published"]["large"]
+    s1, s2 = _sw_inputs("large")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sw_rank, args=(r, 2, port, s1, s2, g["tile_w"], g["tile_h"], q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for _, score, tiles in res:
+        assert score == g["score"]
+        assert tiles == (len(s1) // g["tile_w"]) * (len(s2) // g["tile_h"])
+
+
 def test_atomic_calibration_shapes():
     """The three L2 atomic shapes run and rank as the hardware must: a single
     hot word is far slower than atomics spread over many lines, and the
