@@ -54,6 +54,7 @@ struct SwCtx {
     // 1..nth*th (the left band's right column; null when j0 == 0);
     // right_out receives H of matrix column j1*tw (null: not wanted)
     int j0, j1, i0, i1;
+    int progressive;  // row schedule: chunked bottom-row hand-off
     const int *left_in;  // [nth*th]
     int *right_out;      // [nth*th]
 };
@@ -96,7 +97,7 @@ __device__ __forceinline__ unsigned long long sw_stamp() {
 // keeps the left neighbour's right column in LDS (lds_left, H values) and the
 // top row is the up neighbour's granules, swept until every tag is set;
 // `corner` carries H at (R0-1, C0-1) in and the up tile's bottom-right out.
-template <bool ROWS>
+template <bool ROWS, bool PROG = false>
 __device__ bool sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, int8_t *lds_s1,
                         const int *lds_left, int *lds_right, int &corner, unsigned long long *ph) {
     unsigned long long ts = sw_stamp();
@@ -113,6 +114,13 @@ __device__ bool sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
     const int tw = c.tw, th = c.th;
     const int R0 = (i - 1) * th + 1, C0 = (j - 1) * tw + 1;  // matrix index of cell (0,0)
     const uint32_t tup = t - (uint32_t)c.ntw, tleft = t - 1, tdiag = t - (uint32_t)c.ntw - 1;
+    // progressive bottom-row hand-off (row schedule, one 256-row band, whole
+    // 64-column chunks): the tile publishes each chunk of its bottom row as
+    // soon as its last lane has computed it, and the tile below starts after
+    // the first chunk instead of the whole row (HCLIB_HIP_SW_PROGRESSIVE=0
+    // publishes at the end, as before)
+    const bool prog_out = ROWS && PROG && th == 64 * kSwRP && (tw & 63) == 0;
+    const bool prog = prog_out && i > 1;
     // s1 segment of this tile column
     for (int q = lane; q < tw; q += 64) lds_s1[q] = c.s1[(size_t)(j - 1) * tw + q];
     // v_perm selectors of the 4x4-blocked band: byte k of word b = s1 code - 1
@@ -128,13 +136,16 @@ __device__ bool sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
             for (int q = lane; q < tw; q += 64) lds_top[q + 1] = -((j - 1) * tw + q + 1) + (R0 - 1) + (C0 + q);
             corner = -(j * tw);  // bottom_right of boundary tile (0, j), smith_waterman.cpp:151
         } else {
-            // sweep the up tile's granules until every tag is set (bounded)
+            // sweep the up tile's granules until every tag is set (bounded);
+            // progressive: only the first 64-column chunk, the rest is
+            // fetched inside the step loop as the up tile publishes it
             const unsigned long long *g = c.gbot + (size_t)tup * tw;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            const int qend = prog ? 64 : tw;
             bool all = false;
             while (!all) {
                 bool ok = true;
-                for (int q = lane; q < tw; q += 64) {
+                for (int q = lane; q < qend; q += 64) {
                     const unsigned long long x = ld_agent(&g[q]);
                     if ((x >> 32) != 1ull) ok = false;
                     else lds_top[q + 1] = (int)(uint32_t)x + (R0 - 1) + (C0 + q);
@@ -149,7 +160,7 @@ __device__ bool sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
                 }
             }
             // the next tile's diagonal corner: the up tile's bottom-right
-            corner = (int)(uint32_t)ld_agent(&g[tw - 1]);
+            if (!prog || tw == 64) corner = (int)(uint32_t)ld_agent(&g[tw - 1]);
         }
     } else {
         if (lane == 0) {
@@ -249,7 +260,9 @@ __device__ bool sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
             uint32_t sel_n = lds_sel[cbn];
             int t0n = lds_top[4 * cbn + 1], t1n = lds_top[4 * cbn + 2], t2n = lds_top[4 * cbn + 3],
                 t3n = lds_top[4 * cbn + 4];
-            for (int st = 0; st < nsteps; ++st) {
+            unsigned long long pf = 0;  // prefetched granule of the up tile (progressive)
+            // one anti-diagonal step of the 4x4-blocked band
+            auto step = [&](const int st) {
                 const int blk = st - lane;
                 const bool valid = blk >= 0 && blk < nblocks;
                 const uint32_t sel = sel_n;
@@ -295,6 +308,43 @@ __device__ bool sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
                         bp[1] = o1;
                         bp[2] = o2;
                         bp[3] = o3;
+                    }
+                }
+            };
+            if (!prog_out) {
+                for (int st = 0; st < nsteps; ++st) step(st);
+            } else {
+                // progressive: the hand-off work sits between 16-step runs,
+                // after every step st = 16m + 14 (chunk k is published after
+                // step 16k + 78 and the up tile's chunk k is needed from step
+                // 16k - 1 on), so the step loop itself stays free of it
+                if (prog) pf = ld_agent(&c.gbot[(size_t)tup * tw + 64 + lane]);  // chunk 1
+                for (int base = -1; base < nsteps; base += 16) {
+                    const int lo = base < 0 ? 0 : base, hi = (base + 16) < nsteps ? base + 16 : nsteps;
+                    for (int st = lo; st < hi; ++st) step(st);
+                    const int st = hi - 1;  // = 16m + 14 (nsteps = 16n + 15)
+                    const int pk = st - 78;
+                    if (pk >= 0) {
+                        const int q = 4 * pk + lane;  // chunk pk/16 of this tile's bottom row
+                        st_agent(&c.gbot[(size_t)t * tw + q],
+                                 (1ull << 32) | (unsigned long long)(uint32_t)(lds_bot[q + 1] - (R0 + th - 1) - (C0 + q)));
+                    }
+                    const int kc = st + 2;  // 16k: the up tile's chunk k is due
+                    if (prog && (kc >> 4) < nblocks / 16) {
+                        const int q = 4 * kc + lane;
+                        const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+                        while (!__all((pf >> 32) == 1ull)) {
+                            if (__builtin_amdgcn_s_memrealtime() - w0 > 100000ull * c.spin_ms) {
+                                if (lane == 0) dev_error(c.err, kErrSpinTimeout);
+                                return false;
+                            }
+                            pf = ld_agent(&c.gbot[(size_t)tup * tw + q]);
+                        }
+                        lds_top[q + 1] = (int)(uint32_t)pf + (R0 - 1) + (C0 + q);
+                        if (q + 64 - lane == tw)  // last chunk: the next tile's corner
+                            corner = (int)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pf, 63);
+                        else  // prefetch the next chunk, due 16 steps later
+                            pf = ld_agent(&c.gbot[(size_t)tup * tw + q + 64]);
                     }
                 }
             }
@@ -353,12 +403,12 @@ __device__ bool sw_tile(const SwCtx &c, uint32_t t, int *lds_top, int *lds_bot, 
         __syncthreads();
     }
     const int Rb = R0 + th - 1;  // matrix row of the tile's bottom row
-    if (ROWS) {
+    if (ROWS && !prog_out) {
         // publish: one 8-byte sc1 granule per value (tag 1 = put), drained
         for (int q = lane; q < tw; q += 64)
             st_agent(&c.gbot[(size_t)t * tw + q],
                      (1ull << 32) | (unsigned long long)(uint32_t)(lds_top[q + 1] - Rb - (C0 + q)));
-    } else {
+    } else if (!ROWS) {
         for (int q = lane; q < tw; q += 64)
             st_agent(&c.bottom[(size_t)t * tw + q], lds_top[q + 1] - Rb - (C0 + q));
         if (lane == 0) st_agent(&c.corner[t], lds_top[tw] - Rb - (C0 + tw - 1));
@@ -443,6 +493,7 @@ __global__ __launch_bounds__(64) void k_sw(SwCtx c) {
 // diagonal one is implied (the up row's owner finished (i-1, j-1) before
 // (i-1, j)). Every wave is resident (grid <= CUs) and rows complete in
 // order, so each wait ends.
+template <bool PROG>
 __global__ __launch_bounds__(64) void k_sw_rows(SwCtx c) {
     extern __shared__ __attribute__((aligned(16))) int sw_lds[];
     int *lds_top = sw_lds;
@@ -466,7 +517,7 @@ __global__ __launch_bounds__(64) void k_sw_rows(SwCtx c) {
         for (int j = c.j0; j < c.j1 && ok; ++j) {
             const uint32_t t = (uint32_t)(i * c.ntw + j);
             const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-            ok = sw_tile<true>(c, t, lds_top, lds_bot, lds_s1, lds_left, lds_right, corner, ph);
+            ok = sw_tile<true, PROG>(c, t, lds_top, lds_bot, lds_s1, lds_left, lds_right, corner, ph);
             vm_drain();  // every granule of this tile is out before the next one is computed
             int *tmp = lds_left;  // this tile's right column is the next tile's left
             lds_left = lds_right;
@@ -591,6 +642,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     c.i1 = (int)nth;
     c.left_in = nullptr;
     c.right_out = nullptr;
+    c.progressive = env_int("HCLIB_HIP_SW_PROGRESSIVE", 1);
     int rc = HCLIB_HIP_OK;
     auto fail = [&](int r) { (void)hipFree(d); return r; };
     if ((rc = hip_check(hipMemcpyAsync((void *)c.s1, s1, b_s1, hipMemcpyHostToDevice, m.stream), "copy s1"))) return fail(rc);
@@ -616,7 +668,8 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     if (wpc < 1) wpc = 1;
     int grid = m.num_cus * wpc;
     if (rows && grid > (int)nth) grid = (int)nth;
-    const void *kern = rows ? (const void *)k_sw_rows : (dag ? (const void *)k_sw_dag : (const void *)k_sw);
+    const void *kern = rows ? (c.progressive ? (const void *)k_sw_rows<true> : (const void *)k_sw_rows<false>)
+                            : (dag ? (const void *)k_sw_dag : (const void *)k_sw);
     if (lds > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hclib_hip_dag_stats_t dst{};
     if (dag) {
@@ -638,7 +691,8 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         if ((rc = hclib_hip_dag_end("hclib_hip_sw (dag)", nullptr, nullptr, &dst))) return fail(rc);
     } else {
         if ((rc = hip_check(hipEventRecord(m.ev0, m.stream), "event"))) return fail(rc);
-        if (rows) hipLaunchKernelGGL(k_sw_rows, dim3(grid), dim3(64), lds, m.stream, c);
+        if (rows && c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), lds, m.stream, c);
+        else if (rows) hipLaunchKernelGGL(k_sw_rows<false>, dim3(grid), dim3(64), lds, m.stream, c);
         else hipLaunchKernelGGL(k_sw, dim3(grid), dim3(64), lds, m.stream, c);
         if ((rc = hip_check(hipGetLastError(), "k_sw launch"))) return fail(rc);
         if ((rc = hip_check(hipEventRecord(m.ev1, m.stream), "event"))) return fail(rc);
@@ -751,6 +805,7 @@ extern "C" int hclib_hip_sw_band_begin(const int8_t *s1, size_t n1, const int8_t
     c.nth = (int)nth;
     c.j0 = j0;
     c.j1 = j1;
+    c.progressive = env_int("HCLIB_HIP_SW_PROGRESSIVE", 1);
     c.spin_ms = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     h->lds = lds;
     h->grid_cap = m.num_cus;
@@ -783,7 +838,8 @@ extern "C" int hclib_hip_sw_band_rows(hclib_hip_sw_band_t *h, int i0, int i1, co
     // each granule wait ends (rows above i0 finished in an earlier launch)
     int grid = i1 - i0;
     if (grid > h->grid_cap) grid = h->grid_cap;
-    hipLaunchKernelGGL(k_sw_rows, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
+    if (c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
+    else hipLaunchKernelGGL(k_sw_rows<false>, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
     return hip_check(hipGetLastError(), "k_sw_rows (band) launch");
 }
 

@@ -274,6 +274,29 @@ def test_sw_both_schedules(golden, sched, monkeypatch):
         assert score == L.sw_score(a, b, tw, th), (n1, n2, tw, th)
 
 
+@pytest.mark.parametrize("progressive", ["0", "1"])
+def test_sw_row_schedule_hand_off_forms(golden, progressive, monkeypatch):
+    """The row schedule's bottom-row hand-off — whole rows at the end of a
+    tile (0) or 64-column chunks as the tile computes them (1, default) —
+    gives the 64K golden and the oracle's scores on grids where the chunked
+    form applies (th = 256, tw % 64 == 0) and where it does not."""
+    monkeypatch.setenv("HCLIB_HIP_SW_SCHED", "rows")
+    monkeypatch.setenv("HCLIB_HIP_SW_PROGRESSIVE", progressive)
+    s1, s2 = _sw_inputs("huge")
+    score, st = H.sw(s1[:65536], s2[:65536], 256, 256)
+    assert score == 128772 and st["tiles"] == 65536
+    rng = np.random.default_rng(23)
+    for (n1, n2, tw, th) in [(4096, 2048, 64, 256), (8192, 1536, 512, 256), (3000, 1000, 192, 256),
+                             (2048, 2048, 256, 128), (1000, 777, 100, 256)]:
+        a = bytes(rng.integers(1, 5, n1, dtype=np.int8).tobytes())
+        b = bytes(rng.integers(1, 5, n2, dtype=np.int8).tobytes())
+        score, _ = H.sw(a, b, tw, th)
+        assert score == L.sw_score(a, b, tw, th), (n1, n2, tw, th)
+    # column bands use the same kernel
+    score, tiles, _ = _sw_bands_in_order(s1[:16384], s2[:16384], 256, 256, 4, 8)
+    assert score == L.sw_score(s1[:16384], s2[:16384], 256, 256)
+
+
 def _sw_bands_in_order(s1, s2, tw, th, nbands, block_rows):
     """Every band of an nbands-way column split, run one after the other on
     cuda:0 through hclib_hip_sw_band_* in blocks of tile rows; band r's left
