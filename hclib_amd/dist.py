@@ -158,13 +158,16 @@ class ShardedSw:
     """One rank's share of a sharded SW run. __init__ uploads the band
     (outside any timed region); run() executes the pipeline once and
     returns (score, tiles over all ranks). `band_factory(s1, s2, tw, th, j0,
-    j1)` defaults to the HIP band; the CPU tests pass a host DP band."""
+    j1)` defaults to the HIP band; the CPU tests pass a host DP band.
+    `group` (default: the world group) carries the exchange; `backend` is
+    that group's backend ("gloo" stages the columns through host memory)."""
 
     def __init__(self, s1: bytes, s2: bytes, tw: int, th: int, rank: int, world: int,
-                 backend: str = "nccl", block_rows: int = 16, band_factory=None, device=None):
+                 backend: str = "nccl", block_rows: int = 16, band_factory=None, device=None,
+                 group=None):
         import torch
 
-        self.rank, self.world, self.backend = rank, world, backend
+        self.rank, self.world, self.backend, self.group = rank, world, backend, group
         self.th = th
         ntw, nth = len(s1) // tw, len(s2) // th
         self.j0, self.j1 = sw_bands(ntw, world)[rank]
@@ -182,19 +185,19 @@ class ShardedSw:
         import torch.distributed as dist
 
         if self.backend == "nccl" or t.device.type == "cpu":
-            dist.recv(t, src=self.rank - 1)
+            dist.recv(t, src=self.rank - 1, group=self.group)
         else:  # gloo carries host tensors only
             h = torch.empty_like(t, device="cpu")
-            dist.recv(h, src=self.rank - 1)
+            dist.recv(h, src=self.rank - 1, group=self.group)
             t.copy_(h)
 
     def _send(self, t):
         import torch.distributed as dist
 
         if self.backend == "nccl" or t.device.type == "cpu":
-            dist.send(t, dst=self.rank + 1)
+            dist.send(t, dst=self.rank + 1, group=self.group)
         else:
-            dist.send(t.cpu(), dst=self.rank + 1)
+            dist.send(t.cpu(), dst=self.rank + 1, group=self.group)
 
     def run(self):
         import torch
@@ -213,7 +216,7 @@ class ShardedSw:
 
         dev = _device(self.backend)
         sc = torch.tensor([corner if self.rank == self.world - 1 else 0], dtype=torch.int64, device=dev)
-        dist.broadcast(sc, src=self.world - 1)
+        dist.broadcast(sc, src=self.world - 1, group=self.group)
         tt = torch.tensor([tiles], dtype=torch.int64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM, group=self.group)
         return int(sc[0]), int(tt[0])
