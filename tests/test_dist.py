@@ -95,7 +95,7 @@ class _HostBand:
         return self.prev[-1], self.tiles
 
 
-def _sw_worker(rank, world, port, s1, s2, tw, th, block_rows, q):
+def _sw_worker(rank, world, port, s1, s2, tw, th, block_rows, q, side_group=False):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     import torch
@@ -103,8 +103,11 @@ def _sw_worker(rank, world, port, s1, s2, tw, th, block_rows, q):
     from hclib_amd import dist
 
     r, w, _ = dist.init_from_env("gloo")
+    # side_group: the exchange on its own group, as bench.py runs it beside
+    # an RCCL world group
+    group = torch.distributed.new_group(backend="gloo") if side_group else None
     job = dist.ShardedSw(s1, s2, tw, th, r, w, "gloo", block_rows, band_factory=_HostBand,
-                         device=torch.device("cpu"))
+                         device=torch.device("cpu"), group=group)
     score, tiles = job.run()
     right = None if job.right is None else job.right.tolist()
     dist.barrier(w, "gloo")
@@ -112,8 +115,8 @@ def _sw_worker(rank, world, port, s1, s2, tw, th, block_rows, q):
     q.put((r, score, tiles, job.j1, right))
 
 
-@pytest.mark.parametrize("world,block_rows", [(2, 2), (3, 1), (3, 5)])
-def test_sharded_sw_pipeline_over_gloo(world, block_rows):
+@pytest.mark.parametrize("world,block_rows,side_group", [(2, 2, False), (3, 1, False), (3, 5, True)])
+def test_sharded_sw_pipeline_over_gloo(world, block_rows, side_group):
     import random
 
     from oracle import loader as L
@@ -125,7 +128,7 @@ def test_sharded_sw_pipeline_over_gloo(world, block_rows):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sw_worker, args=(r, world, port, s1, s2, tw, th, block_rows, q))
+    procs = [ctx.Process(target=_sw_worker, args=(r, world, port, s1, s2, tw, th, block_rows, q, side_group))
              for r in range(world)]
     for p in procs:
         p.start()
