@@ -167,8 +167,9 @@ def cpu_baseline(threads, min_seconds=10.0):
 def cpu_configs(threads, s1, s2, gpu):
     """The same CPU runtime (oracle/, "port") on the other BASELINE configs,
     so each GPU figure has its host-CPU counterpart from the same box and
-    run: fib(30) async/finish, SW 64K tile DAG (promises/futures), forasync
-    triad on 2^26 fp32 (bounded: 768 MiB of host arrays). Best of 2 each."""
+    run: fib(30) async/finish, SW 64K tile DAG (promises/futures), UTS T1
+    (best of 5), forasync triad on 2^26 fp32 (bounded: 768 MiB of host
+    arrays). Best of 2 each unless stated."""
     import ctypes as C
 
     import numpy as np
@@ -193,6 +194,16 @@ def cpu_configs(threads, s1, s2, gpu):
     cells = 65536.0 * 65536.0
     out["sw_64k"] = {"cells_per_s": cells / min(best), "s": min(best),
                      "gpu_over_cpu": gpu["sw_64k"]["cells_per_s"] / (cells / min(best))}
+    # UTS T1 (BASELINE config 2): best of 5 full searches (~4.1 M nodes each)
+    p = L.parse_uts_args(T1)
+    best = []
+    for _ in range(5):
+        nn, lv, d, sec = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
+        assert lib.ohc_uts(threads, C.byref(p), C.byref(nn), C.byref(lv), C.byref(d), C.byref(sec)) == 0
+        assert (nn.value, lv.value, d.value) == T1_GOLD, "CPU T1 miscounted"
+        best.append(sec.value)
+    out["uts_t1"] = {"nodes_per_s": T1_GOLD[0] / min(best), "s": min(best),
+                     "gpu_over_cpu": gpu["uts_t1_1gpu"]["nodes_per_s"] / (T1_GOLD[0] / min(best))}
     n = 1 << 26
     rng = np.random.default_rng(1)
     b = rng.random(n, dtype=np.float32)
