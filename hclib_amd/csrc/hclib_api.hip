@@ -906,6 +906,12 @@ int hclib_get_num_workers(void) {
 
 int hclib_get_current_worker(void) { return 0; }
 
+// src/hclib-runtime.c:1365-1368 (workers_backlog, src/hclib-locality-graph.c:
+// 742-758): tasks queued on the calling worker's deques. Here the caller is
+// the host control thread, whose deque is the help-first ready list; device
+// tasks live in the megakernel's queues only while a launch runs.
+size_t hclib_current_worker_backlog(void) { return rt().ready.size(); }
+
 hclib_locale_t *hclib_get_closest_locale(void) { return &rt().host; }
 
 hclib_locale_t *hclib_hip_gpu_locale(int index) {

@@ -147,6 +147,9 @@ int hclib_get_num_workers(void);
  * a blocking one ends the yield) */
 void hclib_yield(hclib_locale_t *locale);
 int hclib_get_current_worker(void);
+/* inc/hclib.h:61, src/hclib-runtime.c:1365-1368: tasks queued on the calling
+ * worker (the host control thread's ready list) */
+size_t hclib_current_worker_backlog(void);
 hclib_locale_t *hclib_get_closest_locale(void);
 void hclib_print_runtime_stats(FILE *fp);
 

@@ -80,6 +80,22 @@ static void entrypoint(void *arg) {
     hclib_future_t *done = hclib_end_finish_nonblocking();
     hclib_future_wait(done);
     assert(counter == k + 1);
+
+    /* backlog (src/hclib-runtime.c:1365-1368): queued, not yet run tasks on
+     * this worker; the awaiting task is not queued until its future is put */
+    hclib_promise_t *gate = hclib_promise_create();
+    hclib_future_t *gf = hclib_get_future_for_promise(gate);
+    size_t before = hclib_current_worker_backlog();
+    hclib_start_finish();
+    hclib_async(leaf, NULL, NULL, 0, NULL);
+    hclib_async(leaf, NULL, NULL, 0, NULL);
+    hclib_async(leaf, NULL, &gf, 1, NULL);
+    assert(hclib_current_worker_backlog() == before + 2);
+    hclib_promise_put(gate, NULL);
+    assert(hclib_current_worker_backlog() == before + 3);
+    hclib_end_finish();
+    assert(hclib_current_worker_backlog() == before);
+    assert(counter == k + 4);
 }
 
 int main(void) {
