@@ -224,17 +224,23 @@ void run_device_task(hclib_task_t *t) {
     }
 }
 
+// the task the control thread is running (hclib_get_curr_task_info)
+static hclib_task_t *g_curr_task = nullptr;
+
 // execute_task, src/hclib-runtime.c:448-478
 void execute(hclib_task_t *t) {
     Runtime &R = rt();
     Finish *saved = R.current;
+    hclib_task_t *saved_task = g_curr_task;
     R.current = t->finish;
+    g_curr_task = t;
     if (t->device_kind) {
         run_device_task(t);
     } else {
         R.host_tasks++;
         t->fp(t->args);
     }
+    g_curr_task = saved_task;
     R.current = saved;
     check_out(t->finish);
     delete t->extra;
@@ -911,6 +917,87 @@ int hclib_get_current_worker(void) { return 0; }
 // the host control thread, whose deque is the help-first ready list; device
 // tasks live in the megakernel's queues only while a launch runs.
 size_t hclib_current_worker_backlog(void) { return rt().ready.size(); }
+
+// src/hclib-runtime.c:480-486: used / capacity of the caller's deque
+void hclib_default_queue_capacity(int *used, int *capacity) {
+    if (used) *used = (int)rt().ready.size();
+    if (capacity) *capacity = 1 << 20;  // INIT_DEQUE_CAPACITY of the reference
+}
+
+// src/hclib.c:475-480: function and argument of the running task (the
+// root task's when called from the hclib_launch entrypoint)
+void hclib_get_curr_task_info(void (**fp_out)(void *), void **args_out) {
+    if (!g_curr_task) die("hclib_get_curr_task_info: no task is running");
+    if (fp_out) *fp_out = g_curr_task->fp;
+    if (args_out) *args_out = g_curr_task->args;
+}
+
+// src/hclib-runtime.c:1340-1363: run fp(data) on the main context. The host
+// control thread is the main context here (no fibers), so it runs in place.
+void hclib_run_on_main_ctx(void (*fp)(void *), void *data) {
+    if (!fp) die("hclib_run_on_main_ctx: null function");
+    fp(data);
+}
+
+// src/hclib-locality-graph.c:1020-1022, 1056-1100: the master worker's first
+// pop locale and the locale every worker can reach; both are system memory
+hclib_locale_t *hclib_get_master_place(void) { return &rt().host; }
+hclib_locale_t *hclib_get_central_place(void) { return &rt().host; }
+
+// src/hclib-locality-graph.c:1136-1170: nearest locale of one of the types,
+// breadth-first from `locale`; the graph here is host <-> bound GPU
+hclib_locale_t *hclib_get_closest_locale_of_types(hclib_locale_t *locale, int *types, int ntypes) {
+    const int n = hclib_get_num_locales();
+    hclib_locale_t *order[2] = {locale, locale == hclib_get_locale(0) ? hclib_get_locale(1) : hclib_get_locale(0)};
+    for (int k = 0; k < 2 && k < n; ++k)
+        for (int q = 0; q < ntypes; ++q)
+            if (order[k] && order[k]->type == types[q]) return order[k];
+    return nullptr;
+}
+hclib_locale_t *hclib_get_closest_locale_of_type(hclib_locale_t *locale, int type) {
+    return hclib_get_closest_locale_of_types(locale, &type, 1);
+}
+
+// src/hclib-locality-graph.c:917-940: each worker's private (first pop)
+// locale; one worker, the control thread, whose locale is system memory
+hclib_locale_t **hclib_get_thread_private_locales(void) {
+    hclib_locale_t **v = (hclib_locale_t **)malloc(sizeof(hclib_locale_t *));
+    if (!v) die("out of memory");
+    v[0] = &rt().host;
+    return v;
+}
+
+// src/hclib-locality-graph.c:829-837
+void hclib_locale_mark_special(hclib_locale_t *locale, const char *special_type) {
+    if (!locale || !special_type) die("hclib_locale_mark_special: null argument");
+    if (locale->special_type) {
+        if (strcmp(locale->special_type, special_type) != 0)
+            die("hclib_locale_mark_special: locale already marked '%s'", locale->special_type);
+    } else {
+        locale->special_type = special_type;
+    }
+}
+
+// src/hclib.c:16-30 and src/hclib-runtime.c:231-239, 396: loop distribution
+// functions; id 0 (HCLIB_DEFAULT_LOOP_DIST) places every tile at the central
+// place
+static hclib_locale_t *default_dist_func(const int, const hclib_loop_domain_t *, const hclib_loop_domain_t *,
+                                         const int) {
+    return hclib_get_central_place();
+}
+static std::vector<loop_dist_func> &dist_funcs() {
+    static std::vector<loop_dist_func> v{default_dist_func};
+    return v;
+}
+unsigned hclib_register_dist_func(loop_dist_func func) {
+    if (!func) die("hclib_register_dist_func: null function");
+    dist_funcs().push_back(func);
+    return (unsigned)dist_funcs().size() - 1;
+}
+loop_dist_func hclib_lookup_dist_func(unsigned id) {
+    if (id >= dist_funcs().size()) die("hclib_lookup_dist_func: no function %u", id);
+    return dist_funcs()[id];
+}
 
 hclib_locale_t *hclib_get_closest_locale(void) { return &rt().host; }
 

@@ -188,6 +188,29 @@ hclib_locale_t *hclib_get_locale(int index); /* 0 = host, 1.. = GPUs */
 hclib_locale_t *hclib_get_all_locales(void);  /* contiguous, hclib_get_num_locales() long */
 int hclib_get_num_locales_of_type(int locale_type);
 hclib_locale_t **hclib_get_all_locales_of_type(int type, int *out_count); /* malloc'd */
+/* locality queries (src/hclib-locality-graph.c:829-837, 917-940, 1020-1022,
+ * 1056-1170) over this runtime's graph: host system memory <-> bound GPU */
+hclib_locale_t *hclib_get_master_place(void);
+hclib_locale_t *hclib_get_central_place(void);
+hclib_locale_t *hclib_get_closest_locale_of_type(hclib_locale_t *locale, int locale_type);
+hclib_locale_t *hclib_get_closest_locale_of_types(hclib_locale_t *locale, int *locale_types, int n_locale_types);
+hclib_locale_t **hclib_get_thread_private_locales(void); /* malloc'd, one per worker */
+void hclib_locale_mark_special(hclib_locale_t *locale, const char *special_type);
+
+/* loop distribution functions (inc/hclib-task.h:71-72, inc/hclib.h:93-95);
+ * id HCLIB_DEFAULT_LOOP_DIST places every tile at the central place */
+typedef hclib_locale_t *(*loop_dist_func)(const int, const hclib_loop_domain_t *, const hclib_loop_domain_t *,
+                                          const int);
+#ifndef HCLIB_DEFAULT_LOOP_DIST
+#define HCLIB_DEFAULT_LOOP_DIST 0
+#endif
+unsigned hclib_register_dist_func(loop_dist_func func);
+loop_dist_func hclib_lookup_dist_func(unsigned id);
+
+/* inc/hclib.h:89, 253, 262 */
+void hclib_run_on_main_ctx(void (*fp)(void *), void *data);
+void hclib_get_curr_task_info(void (**fp_out)(void *), void **args_out);
+void hclib_default_queue_capacity(int *used, int *capacity);
 
 void hclib_register_alloc_func(int locale_type, hclib_module_alloc_impl_func_type func);
 void hclib_register_realloc_func(int locale_type, hclib_module_realloc_impl_func_type func);

@@ -4,6 +4,7 @@
  * test/c/promise/future0.c (a chain of hclib_async_future) and
  * test/c/finish1.c-style nested finish counting. Prints "Check results: OK". */
 #include <assert.h>
+#include <string.h>
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -39,6 +40,20 @@ static void spawner(void *arg) {
     hclib_end_finish();
     assert(counter == n);
 }
+
+static void info_fct(void *arg) {
+    void (*fp)(void *) = NULL;
+    void *a = NULL;
+    hclib_get_curr_task_info(&fp, &a);
+    assert(fp == info_fct && a == arg);
+    counter++;
+}
+static hclib_locale_t *my_dist(const int dim, const hclib_loop_domain_t *sub, const hclib_loop_domain_t *all,
+                               const int mode) {
+    (void)dim; (void)sub; (void)all; (void)mode;
+    return hclib_get_master_place();
+}
+static void on_main(void *arg) { *(int *)arg = 42; }
 
 static void entrypoint(void *arg) {
     (void)arg;
@@ -96,6 +111,37 @@ static void entrypoint(void *arg) {
     hclib_end_finish();
     assert(hclib_current_worker_backlog() == before);
     assert(counter == k + 4);
+
+    /* task info, queue capacity, main context, locality queries, loop
+     * distribution functions (inc/hclib.h:87-95, 253-262) */
+    static int token;
+    hclib_start_finish();
+    hclib_async(info_fct, &token, NULL, 0, NULL);
+    int used = -1, cap = -1;
+    hclib_default_queue_capacity(&used, &cap);
+    assert(used == (int)hclib_current_worker_backlog() && used >= 1 && cap == 1 << 20);
+    hclib_end_finish();
+    assert(counter == k + 5);
+    int flag = 0;
+    hclib_run_on_main_ctx(on_main, &flag);
+    assert(flag == 42);
+    hclib_locale_t *central = hclib_get_central_place();
+    assert(central == hclib_get_master_place() && central == hclib_get_closest_locale());
+    assert(hclib_get_closest_locale_of_type(central, hclib_get_locale_type(central)) == central);
+    int types[2] = {12345, hclib_get_locale_type(central)};
+    assert(hclib_get_closest_locale_of_types(central, types, 2) == central);
+    assert(hclib_get_closest_locale_of_type(central, 12345) == NULL);
+    hclib_locale_t **priv = hclib_get_thread_private_locales();
+    assert(priv[0] == central);
+    free(priv);
+    hclib_locale_t fresh;
+    memset(&fresh, 0, sizeof(fresh));
+    hclib_locale_mark_special(&fresh, "COMM");
+    hclib_locale_mark_special(&fresh, "COMM");  /* same type again: allowed */
+    assert(strcmp(fresh.special_type, "COMM") == 0);
+    assert(hclib_lookup_dist_func(HCLIB_DEFAULT_LOOP_DIST)(1, NULL, NULL, 0) == central);
+    unsigned id = hclib_register_dist_func(my_dist);
+    assert(id >= 1 && hclib_lookup_dist_func(id) == my_dist);
 }
 
 int main(void) {
