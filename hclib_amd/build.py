@@ -26,7 +26,8 @@ LIB = os.path.join(OUT, "libhclib_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["module.hip", "forasync.hip", "uts.hip", "fib.hip", "sw.hip", "dag.hip", "hclib_api.hip", "calib.hip"]
+SOURCES = ["module.hip", "forasync.hip", "uts.hip", "fib.hip", "sw.hip", "dag.hip", "hclib_api.hip", "locality.hip",
+           "calib.hip"]
 CFLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
     "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result",
@@ -79,7 +80,7 @@ def build(verbose: bool = True, variant: str = "") -> str:
     key = "|".join(objs)
     if not os.path.exists(lib) or not os.path.exists(stamp) or open(stamp).read() != key:
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + [
-            "-lpthread"]
+            "-lpthread", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")

@@ -291,8 +291,12 @@ extern "C" int hclib_hip_forasync(int body, const void *args, int dim,
         A.total *= pre[d].back();
     }
     if (A.total == 0) return HCLIB_HIP_OK;
+    hipStream_t st = (hipStream_t)stream;
+    // the run table is stream-ordered memory: allocated, uploaded, used and
+    // freed in the launch's stream order, so the call never waits for the
+    // sweep (a forasync inside a finish completes when the finish ends)
     char *dbuf = nullptr;
-    HX_HIP(hipMalloc((void **)&dbuf, bytes));
+    HX_HIP(hipMallocAsync((void **)&dbuf, bytes, st));
     std::vector<char> hbuf(bytes);
     size_t off = 0;
     for (int d = 0; d < dim; ++d) {
@@ -304,15 +308,13 @@ extern "C" int hclib_hip_forasync(int body, const void *args, int dim,
         off += (pre[d].size() * 8 + 15) & ~(size_t)15;
         A.dim[d].nruns = (int)runs[d].size();
     }
-    hipStream_t st = (hipStream_t)stream;
+    // pageable source: the copy has consumed hbuf when it returns
     HX_HIP(hipMemcpyAsync(dbuf, hbuf.data(), bytes, hipMemcpyHostToDevice, st));
     int64_t grid = (A.total + 255) / 256;
     const int64_t maxg = (int64_t)mod().num_cus * 16;
     if (grid > maxg) grid = maxg;
     hipLaunchKernelGGL(k_forasync_sweep, dim3((unsigned)grid), dim3(256), 0, st, A);
     HX_HIP(hipGetLastError());
-    // the run table must outlive the launch
-    HX_HIP(hipStreamSynchronize(st));
-    HX_HIP(hipFree(dbuf));
+    HX_HIP(hipFreeAsync(dbuf, st));
     return HCLIB_HIP_OK;
 }

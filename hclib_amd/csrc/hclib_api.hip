@@ -18,8 +18,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 #include <ucontext.h>
+#include <unistd.h>
 
 #include <map>
 #include <string>
@@ -27,27 +29,19 @@
 
 #include "../../include/hclib.h"
 #include "../../include/hclib_forasync_sets.h"
+#include "hx_host.h"
 #include "hx_module.h"
 
+using hxh::die;
 
 // finish_t, src/inc/hclib-finish.h:6-10
-struct Finish {
-    Finish *parent;
+struct finish_t {
+    finish_t *parent;
     int counter;
     hclib_promise_t *finish_dep;
 };
 
-struct hclib_task_t {
-    generic_frame_ptr fp;
-    void *args;
-    Finish *finish;
-    hclib_future_t *waiting_on[MAX_NUM_WAITS];
-    std::vector<hclib_future_t *> *extra;
-    int waiting_on_index;
-    int device_kind;  // 0 = host task
-    int non_blocking; // hclib_async_nb (src/hclib.c:51-57)
-    hclib_task_t *next_waiter;
-};
+static_assert(sizeof(hclib_task_t) == 96, "hclib_task_t keeps the reference's 96-byte layout");
 
 namespace {
 
@@ -57,19 +51,10 @@ namespace {
 struct Runtime {
     bool launched = false;
     bool hip = false;
-    Finish *current = nullptr;
     std::vector<hclib_task_t *> ready;  // LIFO, like the owner end of a deque
     std::map<generic_frame_ptr, int> kinds;
     std::map<void *, int> bodies;
-    // [0] = the host ("sysmem"), [1] = this process's GPU ("GPU"): one array,
-    // as hclib_get_all_locales hands it out
-    hclib_locale_t locales[2] = {{0, 0, "sysmem", "sysmem", nullptr, nullptr, 0, 1, nullptr},
-                                 {1, 1, "GPU0", "GPU", nullptr, nullptr, 0, 1, nullptr}};
-    hclib_locale_t &host = locales[0];
-    hclib_locale_t &gpu = locales[1];
-    int gpu_index = 0;
-    // locale types and their memory callbacks (src/hclib-mem.c:13-50)
-    std::vector<std::string> types{"sysmem", "GPU"};
+    // memory callbacks per locale type (src/hclib-mem.c:13-50)
     struct MemFuncs {
         hclib_module_alloc_impl_func_type alloc = nullptr;
         hclib_module_realloc_impl_func_type realloc = nullptr;
@@ -92,32 +77,15 @@ Runtime &rt() {
     return r;
 }
 
-[[noreturn]] void die(const char *fmt, ...) {
-    va_list ap;
-    va_start(ap, fmt);
-    fprintf(stderr, "hclib: ");
-    vfprintf(stderr, fmt, ap);
-    fprintf(stderr, "\n");
-    va_end(ap);
-    abort();
-}
+// the finish scope and the task the host worker is running
+inline finish_t *&current_finish() { return hxh::worker0()->current_finish; }
+inline hclib_task_t *current_task() { return (hclib_task_t *)hxh::worker0()->curr_task; }
 
-struct ModuleHooks {
-    std::string name;
-    hclib_module_pre_init_func_type pre;
-    hclib_module_post_init_func_type post;
-    hclib_module_finalize_func_type fin;
-};
-std::vector<ModuleHooks> &modules() {
-    static std::vector<ModuleHooks> m;
-    return m;
-}
-
-void check_in(Finish *f) {
+void check_in(finish_t *f) {
     if (f) f->counter++;
 }
 
-void check_out(Finish *f) {
+void check_out(finish_t *f) {
     if (f && --f->counter == 0 && f->finish_dep) hclib_promise_put(f->finish_dep, f);
 }
 
@@ -130,17 +98,21 @@ bool register_if_not_ready(hclib_task_t *t, hclib_future_t *fut) {
     return true;
 }
 
-// register_on_all_promise_dependencies, src/hclib-promise.c:171-195
+// register_on_all_promise_dependencies, src/hclib-promise.c:171-195: the
+// inline futures (NULL-terminated unless all four are used), then the
+// NULL-terminated waiting_on_extra
 bool register_all(hclib_task_t *t) {
     while (t->waiting_on_index < MAX_NUM_WAITS - 1) {
         t->waiting_on_index++;
         hclib_future_t *f = t->waiting_on[t->waiting_on_index];
-        if (f && register_if_not_ready(t, f)) return false;
+        if (!f) return true;
+        if (register_if_not_ready(t, f)) return false;
     }
-    if (t->extra) {
-        while (t->waiting_on_index - MAX_NUM_WAITS + 1 < (int)t->extra->size()) {
+    if (t->waiting_on_extra) {
+        while (true) {
+            hclib_future_t *f = t->waiting_on_extra[t->waiting_on_index - MAX_NUM_WAITS + 1];
+            if (!f) break;
             t->waiting_on_index++;
-            hclib_future_t *f = (*t->extra)[t->waiting_on_index - MAX_NUM_WAITS];
             if (register_if_not_ready(t, f)) return false;
         }
     }
@@ -154,16 +126,24 @@ int check_hip(int rc, const char *what) {
     return rc;
 }
 
-void ensure_gpu(const char *who) {
+// bind the hip module (modules/hip) to `device` (-1: the process's default,
+// HCLIB_HIP_DEVICE or LOCAL_RANK). One GPU per process: a second device is
+// an error, as one rank drives one GPU in the multi-GPU launch.
+void ensure_gpu(const char *who, int device = -1) {
+    if (device < 0) device = hx::env_int("HCLIB_HIP_DEVICE", hx::env_int("LOCAL_RANK", 0));
     if (!rt().hip) {
-        // device kinds need the "hip" module; load it on first use, as the
-        // reference dlopens modules named in deps (src/hclib-runtime.c:294-317)
-        if (hclib_hip_init(hx::env_int("HCLIB_HIP_DEVICE", hx::env_int("LOCAL_RANK", 0))) !=
-            HCLIB_HIP_OK)
-            die("%s: the hip module could not bind a gfx950 device: %s", who,
-                hclib_hip_last_error());
+        if (hclib_hip_init(device) != HCLIB_HIP_OK)
+            die("%s: the hip module could not bind a gfx950 device: %s", who, hclib_hip_last_error());
         rt().hip = true;
+    } else if (hx::mod().device != device) {
+        die("%s: this process drives GPU %d; GPU %d needs a process of its own", who, hx::mod().device, device);
     }
+}
+
+// the device a task at `locale` runs on (-1: the process's default)
+int device_of(hclib_locale_t *locale) {
+    const int d = hxh::locale_device(locale);
+    return d;
 }
 
 // the megakernel's scheduler counters of the launch that just ended
@@ -176,12 +156,19 @@ void add_sched_counters(Runtime &R) {
     R.device_chunks_stolen += c[15];
 }
 
-// run one device task kind to completion and write its outputs back
-void run_device_task(hclib_task_t *t) {
+int kind_of(generic_frame_ptr fp) {
     Runtime &R = rt();
-    ensure_gpu("device task");
+    if (R.kinds.empty()) return 0;
+    auto k = R.kinds.find(fp);
+    return k == R.kinds.end() ? 0 : k->second;
+}
+
+// run one device task kind to completion and write its outputs back
+void run_device_task(hclib_task_t *t, int kind) {
+    Runtime &R = rt();
+    ensure_gpu("device task", device_of(t->locale));
     R.device_tasks++;
-    switch (t->device_kind) {
+    switch (kind) {
     case HCLIB_HIP_KIND_FIB: {
         // FibArgs of test/fib/fib.c:50-53: { int n; long res; }
         struct FibArgs {
@@ -220,85 +207,178 @@ void run_device_task(hclib_task_t *t) {
         break;
     }
     default:
-        die("unknown device task kind %d", t->device_kind);
+        die("unknown device task kind %d", kind);
     }
 }
 
-// the task the control thread is running (hclib_get_curr_task_info)
-static hclib_task_t *g_curr_task = nullptr;
+// the root task of hclib_launch: its record carries the user's function and
+// argument (hclib_get_curr_task_info reports them, as the reference's root
+// async does, src/hclib-runtime.c:1472) but it runs on a context of its own
+hclib_task_t *g_root_task = nullptr;
+void run_root(hclib_task_t *t);
 
 // execute_task, src/hclib-runtime.c:448-478
 void execute(hclib_task_t *t) {
     Runtime &R = rt();
-    Finish *saved = R.current;
-    hclib_task_t *saved_task = g_curr_task;
-    R.current = t->finish;
-    g_curr_task = t;
-    if (t->device_kind) {
-        run_device_task(t);
+    hclib_worker_state *ws = hxh::worker0();
+    finish_t *saved = ws->current_finish;
+    void *saved_task = ws->curr_task;
+    ws->current_finish = t->current_finish;
+    ws->curr_task = t;
+    if (t == g_root_task) {
+        R.host_tasks++;
+        run_root(t);
+    } else if (const int kind = kind_of(t->_fp)) {
+        run_device_task(t, kind);
     } else {
         R.host_tasks++;
-        t->fp(t->args);
+        t->_fp(t->args);
     }
-    g_curr_task = saved_task;
-    R.current = saved;
-    check_out(t->finish);
-    delete t->extra;
-    free(t);
+    ws->curr_task = saved_task;
+    ws->current_finish = saved;
+    check_out(t->current_finish);
+    free(t->waiting_on_extra);
+    if (t != g_root_task) free(t);
 }
 
-// find_and_run_task with one worker: pop the newest ready task
+// Device work in flight on the module stream that belongs to a finish scope
+// (a device forasync): the scope stays checked in until the work's event
+// completes, like the pending operations modules/cuda polls
+// (modules/common/hclib-module-common.h:10-90). The host worker completes
+// them while it helps: finished ones first, and when it has no ready task
+// left it waits for the oldest.
+struct DeviceOp {
+    hipEvent_t ev;
+    finish_t *finish;
+    void (*done)(void *);
+    void *arg;
+};
+std::vector<DeviceOp> &pending() {
+    static std::vector<DeviceOp> p;
+    return p;
+}
+
+void complete_op(size_t i) {
+    DeviceOp op = pending()[i];
+    pending().erase(pending().begin() + (ptrdiff_t)i);
+    (void)hipEventDestroy(op.ev);
+    if (op.done) op.done(op.arg);
+    check_out(op.finish);
+}
+
+// returns true if any operation completed
+bool poll_pending(bool wait_oldest) {
+    std::vector<DeviceOp> &P = pending();
+    if (P.empty()) return false;
+    if (wait_oldest) {
+        if (hipEventSynchronize(P[0].ev) != hipSuccess) die("device work of a finish scope failed");
+        complete_op(0);
+        return true;
+    }
+    bool any = false;
+    for (size_t i = 0; i < P.size();) {
+        const hipError_t e = hipEventQuery(P[i].ev);
+        if (e == hipSuccess) {
+            complete_op(i);
+            any = true;
+        } else if (e == hipErrorNotReady) {
+            ++i;
+        } else {
+            die("device work of a finish scope failed: %s", hipGetErrorString(e));
+        }
+    }
+    return any;
+}
+
+// register device work just enqueued on `stream` with the current finish
+void add_device_op(hipStream_t stream, void (*done)(void *), void *arg) {
+    DeviceOp op{nullptr, current_finish(), done, arg};
+    if (hipEventCreateWithFlags(&op.ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(op.ev, stream) != hipSuccess)
+        die("cannot record device work");
+    check_in(op.finish);
+    pending().push_back(op);
+}
+
+// find_and_run_task with one worker: complete finished device work, pop
+// the newest ready task; with nothing ready, wait for the oldest device work
 bool run_one() {
     Runtime &R = rt();
-    if (R.ready.empty()) return false;
+    poll_pending(false);
+    if (R.ready.empty()) return poll_pending(true);
     hclib_task_t *t = R.ready.back();
     R.ready.pop_back();
     execute(t);
     return true;
 }
 
-void spawn(generic_frame_ptr fp, void *arg, hclib_future_t **futures, int nfutures,
-           int non_blocking = 0) {
+// spawn_handler, src/hclib-runtime.c:572-617: check in on the current
+// finish (escaping tasks do not), copy the futures (extras into a
+// NULL-terminated waiting_on_extra), schedule once all are satisfied
+void spawn_handler(hclib_task_t *t, hclib_locale_t *locale, hclib_future_t **futures, int nfutures,
+                   int escaping) {
     Runtime &R = rt();
-    if (!R.launched) die("hclib_async called outside hclib_launch");
+    if (!R.launched) die("a task was spawned outside hclib_launch");
+    if (!t) die("spawn: NULL task");
+    if (escaping) {
+        t->current_finish = nullptr;
+    } else {
+        check_in(current_finish());
+        t->current_finish = current_finish();
+    }
+    if (locale) t->locale = locale;
+    R.spawned++;
+    if (nfutures > 0) {
+        const int inl = nfutures > MAX_NUM_WAITS ? MAX_NUM_WAITS : nfutures;
+        memcpy(t->waiting_on, futures, (size_t)inl * sizeof(*futures));
+        if (nfutures > MAX_NUM_WAITS) {
+            const int extra = nfutures - MAX_NUM_WAITS;
+            t->waiting_on_extra = (hclib_future_t **)malloc((size_t)(extra + 1) * sizeof(hclib_future_t *));
+            if (!t->waiting_on_extra) die("out of memory");
+            memcpy(t->waiting_on_extra, futures + MAX_NUM_WAITS, (size_t)extra * sizeof(*futures));
+            t->waiting_on_extra[extra] = nullptr;
+        }
+        t->waiting_on_index = -1;
+    }
+    // is_eligible_to_schedule, src/hclib-runtime.c:540-551
+    if (!t->waiting_on[0] || register_all(t)) make_ready(t);
+}
+
+hclib_task_t *new_task(generic_frame_ptr fp, void *arg, int non_blocking) {
     hclib_task_t *t = (hclib_task_t *)calloc(1, sizeof(hclib_task_t));
     if (!t) die("out of memory");
-    t->fp = fp;
+    t->_fp = fp;
     t->args = arg;
-    auto k = R.kinds.find(fp);
-    t->device_kind = (k == R.kinds.end()) ? 0 : k->second;
     t->non_blocking = non_blocking;
-    t->finish = R.current;
-    check_in(t->finish);
-    R.spawned++;
-    t->waiting_on_index = -1;
-    for (int i = 0; i < nfutures && i < MAX_NUM_WAITS; ++i) t->waiting_on[i] = futures[i];
-    if (nfutures > MAX_NUM_WAITS) {
-        t->extra = new std::vector<hclib_future_t *>(futures + MAX_NUM_WAITS, futures + nfutures);
-    }
-    if (nfutures == 0 || register_all(t)) make_ready(t);
+    return t;
 }
 
 }  // namespace
 
 namespace {
-struct RootTask {
-    async_fct_t fn;
-    void *arg;
-    void *stack;
-};
+// The root task runs on a context of its own, as the reference's does (a
+// LiteCtx fiber, src/hclib-runtime.c:1460-1478). Its stack is mmap'd with a
+// PROT_NONE guard page below it (the reference's OVERFLOW_PROTECT pad,
+// src/inc/litectx.h:68,117): every host task runs nested on it (help-first
+// inside end_finish / future_wait), and an overflow must fault, not corrupt
+// the heap. It stays mapped until the launch ends, so tasks that outlive the
+// root body and still read its locals (test/cpp/promise/future5.cpp) see
+// them intact.
 constexpr size_t kRootStack = 8u << 20;  // touched lazily
 ucontext_t g_root_ret, g_root_ctx;
-RootTask *g_root = nullptr;
-void root_trampoline() { g_root->fn(g_root->arg); }
-void run_root_on_own_stack(void *raw) {
-    RootTask *r = (RootTask *)raw;
-    r->stack = malloc(kRootStack);
-    if (!r->stack || getcontext(&g_root_ctx) != 0) die("hclib_launch: cannot create the root context");
-    g_root_ctx.uc_stack.ss_sp = r->stack;
+void *g_root_map = nullptr;
+size_t g_root_map_len = 0;
+void root_trampoline() { g_root_task->_fp(g_root_task->args); }
+void run_root(hclib_task_t *) {
+    const size_t page = (size_t)sysconf(_SC_PAGESIZE);
+    g_root_map_len = kRootStack + page;
+    g_root_map = mmap(nullptr, g_root_map_len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE,
+                      -1, 0);
+    if (g_root_map == MAP_FAILED || mprotect(g_root_map, page, PROT_NONE) != 0 || getcontext(&g_root_ctx) != 0)
+        die("hclib_launch: cannot create the root context");
+    g_root_ctx.uc_stack.ss_sp = (char *)g_root_map + page;
     g_root_ctx.uc_stack.ss_size = kRootStack;
     g_root_ctx.uc_link = &g_root_ret;
-    g_root = r;
     makecontext(&g_root_ctx, root_trampoline, 0);
     if (swapcontext(&g_root_ret, &g_root_ctx) != 0) die("hclib_launch: cannot enter the root context");
 }
@@ -307,30 +387,21 @@ void run_root_on_own_stack(void *raw) {
 extern "C" {
 
 // ------------------------------------------------------------ lifecycle
-int hclib_add_module_init_function(const char *lbl, hclib_module_pre_init_func_type pre,
-                                   hclib_module_post_init_func_type post,
-                                   hclib_module_finalize_func_type finalize) {
-    modules().push_back(ModuleHooks{lbl ? lbl : "", pre, post, finalize});
-    return 0;
-}
-
+// hclib_entrypoint, src/hclib-runtime.c:319-401: load the modules named in
+// deps, their pre-init functions, the locality graph, their post-init
+// functions, then the root finish
 void hclib_init(const char **deps, int ndeps, const int instrument) {
     (void)instrument;
     Runtime &R = rt();
     if (R.launched) die("hclib_init called twice");
-    for (auto &m : modules())
-        if (m.pre) m.pre();
-    for (int i = 0; i < ndeps; ++i) {
-        const char *d = deps[i];
-        if (!strcmp(d, "hip") || !strcmp(d, "gpu")) {
-            ensure_gpu("hclib_init");
-        } else if (strcmp(d, "system") != 0) {
-            fprintf(stderr, "WARNING: hclib module \"%s\" is not available in this build\n", d);
-        }
-    }
-    for (auto &m : modules())
-        if (m.post) m.post();
+    hxh::load_dependencies(deps, ndeps);
+    hclib_call_module_pre_init_functions();
+    hxh::bind_worker0();  // builds the graph, makes current_ws() answer here
+    for (int i = 0; i < ndeps; ++i)
+        if (!strcmp(deps[i], "hip") || !strcmp(deps[i], "gpu")) ensure_gpu("hclib_init");
+    hclib_call_module_post_init_functions();
     R.launched = true;
+    current_finish() = nullptr;
     hclib_start_finish();  // root finish (src/hclib-runtime.c:400)
 }
 
@@ -338,8 +409,7 @@ void hclib_finalize(const int instrument) {
     (void)instrument;
     Runtime &R = rt();
     hclib_end_finish();
-    for (auto &m : modules())
-        if (m.fin) m.fin();
+    hclib_call_finalize_functions();
     R.launched = false;
     const char *stats = getenv("HCLIB_STATS");
     if (stats && *stats && strcmp(stats, "0")) hclib_print_runtime_stats(stdout);
@@ -349,14 +419,16 @@ void hclib_launch(async_fct_t fct_ptr, void *arg, const char **deps, int ndeps) 
     const char *prof = getenv("HCLIB_PROFILE_LAUNCH_BODY");
     hclib_init(deps, ndeps, 0);
     const unsigned long long t0 = hclib_current_time_ns();
-    // the root task runs on a context of its own, as the reference's does
-    // (a LiteCtx fiber, src/hclib-runtime.c:1460-1478); its stack stays
-    // mapped until the launch ends, so tasks that outlive the root body and
-    // still read its locals (test/cpp/promise/future5.cpp) see them intact
-    RootTask root{fct_ptr, arg, nullptr};
-    hclib_async(run_root_on_own_stack, &root, nullptr, 0, nullptr);
+    hclib_task_t root;
+    memset(&root, 0, sizeof(root));
+    root._fp = fct_ptr;
+    root.args = arg;
+    g_root_task = &root;
+    spawn_handler(&root, hclib_get_closest_locale(), nullptr, 0, 0);
     hclib_finalize(0);  // ends the root finish: the root task runs here
-    free(root.stack);
+    g_root_task = nullptr;
+    if (g_root_map) munmap(g_root_map, g_root_map_len);
+    g_root_map = nullptr;
     const unsigned long long t1 = hclib_current_time_ns();
     if (prof && *prof) printf("\nHCLIB TIME %llu ns\n", t1 - t0);
 }
@@ -370,15 +442,24 @@ unsigned long long hclib_current_time_ns(void) {
 unsigned long long hclib_current_time_ms(void) { return hclib_current_time_ns() / 1000000ull; }
 
 // ---------------------------------------------------------------- tasks
+// inc/hclib-async-struct.h:49-54, src/hclib-runtime.c:619-644
+void spawn(hclib_task_t *task) { spawn_handler(task, nullptr, nullptr, 0, 0); }
+void spawn_at(hclib_task_t *task, hclib_locale_t *locale) { spawn_handler(task, locale, nullptr, 0, 0); }
+void spawn_await_at(hclib_task_t *task, hclib_future_t **futures, const int nfutures, hclib_locale_t *locale) {
+    spawn_handler(task, locale, futures, nfutures, 0);
+}
+void spawn_await(hclib_task_t *task, hclib_future_t **futures, const int nfutures) {
+    spawn_handler(task, nullptr, futures, nfutures, 0);
+}
+
+// src/hclib.c:34-57
 void hclib_async(generic_frame_ptr fp, void *arg, hclib_future_t **futures, const int nfutures,
                  hclib_locale_t *locale) {
-    (void)locale;  // device kinds run on the GPU locale, everything else on the host
-    spawn(fp, arg, futures, nfutures);
+    spawn_handler(new_task(fp, arg, 0), locale, futures, nfutures, 0);
 }
 
 void hclib_async_nb(generic_frame_ptr fp, void *arg, hclib_locale_t *locale) {
-    (void)locale;
-    spawn(fp, arg, nullptr, 0, 1);
+    spawn_handler(new_task(fp, arg, 1), locale, nullptr, 0, 0);
 }
 
 // hclib_yield, src/hclib-runtime.c:1142-1217, with the control thread as the
@@ -423,18 +504,18 @@ hclib_future_t *hclib_async_future(future_fct_t fp, void *arg, hclib_future_t **
 
 // hclib_start_finish, src/hclib-runtime.c:1219-1247
 void hclib_start_finish(void) {
-    Runtime &R = rt();
-    Finish *f = (Finish *)calloc(1, sizeof(Finish));
+    finish_t *f = (finish_t *)calloc(1, sizeof(finish_t));
+    if (!f) die("out of memory");
     f->counter = 1;
-    f->parent = R.current;
+    f->parent = current_finish();
     check_in(f->parent);
-    R.current = f;
+    current_finish() = f;
 }
 
 // hclib_end_finish + help_finish, src/hclib-runtime.c:1249-1277, 1067-1119
 void hclib_end_finish(void) {
     Runtime &R = rt();
-    Finish *f = R.current;
+    finish_t *f = current_finish();
     if (!f) die("hclib_end_finish without a matching start");
     R.end_finishes++;
     while (f->counter > 1) {
@@ -442,7 +523,7 @@ void hclib_end_finish(void) {
             die("end_finish: %d task(s) wait on promises that nothing can put (deadlock)",
                 f->counter - 1);
     }
-    R.current = f->parent;
+    current_finish() = f->parent;
     check_out(f->parent);
     free(f);
 }
@@ -451,9 +532,10 @@ void hclib_end_finish(void) {
 void hclib_end_finish_nonblocking_helper(hclib_promise_t *event) {
     Runtime &R = rt();
     R.end_finishes_nb++;
-    Finish *f = R.current;
+    finish_t *f = current_finish();
+    if (!f) die("hclib_end_finish_nonblocking without a matching start");
     f->finish_dep = event;
-    R.current = f->parent;
+    current_finish() = f->parent;
     check_out(f);  // the owner's check-out; puts `event` when the scope drains
     check_out(f->parent);
 }
@@ -528,10 +610,29 @@ void forasync_host(void *fct, void *argv, int dim, hclib_loop_domain_t *domain, 
                 t->r[0] = a;
                 t->r[1] = dim > 1 ? runs[1][j] : one;
                 t->r[2] = dim > 2 ? runs[2][k] : one;
-                spawn(host_tile_runner, t, nullptr, 0);
+                spawn_handler(new_task(host_tile_runner, t, 0), nullptr, nullptr, 0, 0);
             }
 }
 
+}  // namespace
+
+namespace {
+struct IotaOp {
+    int *host;
+    size_t n;
+    int *dev_ran, *dev_err;
+};
+void iota_done(void *raw) {
+    IotaOp *op = (IotaOp *)raw;
+    int nerr = 0;
+    if (hipMemcpy(op->host, op->dev_ran, op->n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&nerr, op->dev_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        die("hclib_forasync: copy-back failed");
+    (void)hipFree(op->dev_ran);
+    (void)hipFree(op->dev_err);
+    free(op);
+    if (nerr) die("forasync body check failed at %d indices", nerr);
+}
 }  // namespace
 
 extern "C" {
@@ -551,33 +652,36 @@ void hclib_forasync(void *fct, void *argv, int dim, hclib_loop_domain_t *domain,
     R.forasyncs++;
     static_assert(sizeof(hclib_loop_domain_t) == sizeof(hclib_hip_loop_domain_t), "layout");
     hclib_hip_loop_domain_t *d = (hclib_hip_loop_domain_t *)domain;
+    hipStream_t st = hx::mod().stream;
     int rc;
     if (b->second == HCLIB_HIP_BODY_IOTA_CHECK) {
-        // test/c/forasync1DCh.c passes a plain host int array: map it for the sweep
+        // test/c/forasync1DCh.c passes a plain host int array: the sweep runs
+        // on a device copy, copied back when the sweep completes
         hclib_hip_loop_domain_t dd = d[0];
-        if (dd.tile == -1) dd.tile = ((dd.high - dd.low) + hclib_get_num_workers() - 1) /
-                                     hclib_get_num_workers();
+        const int nw = hclib_hip_num_workers() > 0 ? hclib_hip_num_workers() : 1;
+        if (dd.tile == -1) dd.tile = ((dd.high - dd.low) + nw - 1) / nw;
         const size_t extent = (size_t)(dd.high + (dd.tile > 0 ? dd.tile : 1));
-        int *dev_ran = nullptr, *dev_err = nullptr;
-        if (hipMalloc((void **)&dev_ran, extent * sizeof(int)) != hipSuccess ||
-            hipMalloc((void **)&dev_err, sizeof(int)) != hipSuccess)
+        IotaOp *op = (IotaOp *)calloc(1, sizeof(IotaOp));
+        if (!op) die("out of memory");
+        op->host = (int *)argv;
+        op->n = (size_t)dd.high;
+        if (hipMalloc((void **)&op->dev_ran, extent * sizeof(int)) != hipSuccess ||
+            hipMalloc((void **)&op->dev_err, sizeof(int)) != hipSuccess)
             die("hclib_forasync: device allocation failed");
-        (void)hipMemcpy(dev_ran, argv, (size_t)dd.high * sizeof(int), hipMemcpyHostToDevice);
-        (void)hipMemset(dev_err, 0, sizeof(int));
-        hclib_hip_iota_args_t ia = {dev_ran, dev_err};
-        rc = hclib_hip_forasync(b->second, &ia, dim, d, mode, nullptr);
-        (void)hipDeviceSynchronize();
-        int nerr = 0;
-        (void)hipMemcpy(argv, dev_ran, (size_t)dd.high * sizeof(int), hipMemcpyDeviceToHost);
-        (void)hipMemcpy(&nerr, dev_err, sizeof(int), hipMemcpyDeviceToHost);
-        (void)hipFree(dev_ran);
-        (void)hipFree(dev_err);
-        if (nerr) die("forasync body check failed at %d indices", nerr);
+        if (hipMemcpyAsync(op->dev_ran, argv, op->n * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemsetAsync(op->dev_err, 0, sizeof(int), st) != hipSuccess)
+            die("hclib_forasync: upload failed");
+        hclib_hip_iota_args_t ia = {op->dev_ran, op->dev_err};
+        rc = hclib_hip_forasync(b->second, &ia, dim, d, mode, st);
+        check_hip(rc, "hclib_hip_forasync");
+        add_device_op(st, iota_done, op);
     } else {
-        rc = hclib_hip_forasync(b->second, argv, dim, d, mode, nullptr);
-        (void)hipDeviceSynchronize();  // the sweep belongs to the enclosing finish
+        // the sweep belongs to the enclosing finish: it completes there (or
+        // in whatever helps first), the host thread does not wait for it here
+        rc = hclib_hip_forasync(b->second, argv, dim, d, mode, st);
+        check_hip(rc, "hclib_hip_forasync");
+        add_device_op(st, nullptr, nullptr);
     }
-    check_hip(rc, "hclib_hip_forasync");
 }
 
 hclib_future_t *hclib_forasync_future(void *fct, void *argv, int dim,
@@ -779,55 +883,6 @@ MemTask *new_mem_task(int op, hclib_locale_t *l) {
 
 extern "C" {
 
-int hclib_add_known_locale_type(const char *lbl) {  // src/hclib-locality-graph.c
-    Runtime &R = rt();
-    for (size_t i = 0; i < R.types.size(); ++i)
-        if (R.types[i] == lbl) return (int)i;
-    R.types.push_back(lbl);
-    return (int)R.types.size() - 1;
-}
-
-int hclib_get_locale_type(hclib_locale_t *l) { return check_locale(l, "hclib_get_locale_type")->type; }
-
-const char *hclib_get_locale_type_name(int type) {
-    Runtime &R = rt();
-    return (type >= 0 && type < (int)R.types.size()) ? R.types[type].c_str() : nullptr;
-}
-
-int hclib_get_num_locales(void) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
-    return 1 + (n > 0 ? 1 : 0);  // the host and the bound GPU (one GPU per process)
-}
-
-hclib_locale_t *hclib_get_locale(int index) {
-    Runtime &R = rt();
-    if (index == 0) return &R.host;
-    if (index == 1 && hclib_get_num_locales() > 1) return &R.gpu;
-    return nullptr;
-}
-
-hclib_locale_t *hclib_get_all_locales(void) { return rt().locales; }
-
-int hclib_get_num_locales_of_type(int type) {
-    int n = 0;
-    hclib_locale_t **v = hclib_get_all_locales_of_type(type, &n);
-    free(v);
-    return n;
-}
-
-hclib_locale_t **hclib_get_all_locales_of_type(int type, int *out_count) {
-    const int n = hclib_get_num_locales();
-    hclib_locale_t **v = (hclib_locale_t **)malloc(sizeof(hclib_locale_t *) * (size_t)(n + 1));
-    int k = 0;
-    for (int i = 0; i < n; ++i) {
-        hclib_locale_t *l = hclib_get_locale(i);
-        if (l && (int)l->type == type) v[k++] = l;
-    }
-    if (out_count) *out_count = k;
-    return v;
-}
-
 // hclib_register_*_func, src/hclib-mem.c:23-50 (alloc/realloc/free/memset are MAY_USE)
 void hclib_register_alloc_func(int t, hclib_module_alloc_impl_func_type f) { mem_of(t).alloc = f; }
 void hclib_register_realloc_func(int t, hclib_module_realloc_impl_func_type f) { mem_of(t).realloc = f; }
@@ -905,13 +960,6 @@ hclib_future_t *hclib_async_copy(hclib_locale_t *dst_locale, void *dst, hclib_lo
 extern "C" {
 
 // -------------------------------------------------------------- queries
-int hclib_get_num_workers(void) {
-    const int n = hclib_hip_num_workers();
-    return n > 0 ? n : 1;
-}
-
-int hclib_get_current_worker(void) { return 0; }
-
 // src/hclib-runtime.c:1365-1368 (workers_backlog, src/hclib-locality-graph.c:
 // 742-758): tasks queued on the calling worker's deques. Here the caller is
 // the host control thread, whose deque is the help-first ready list; device
@@ -927,9 +975,10 @@ void hclib_default_queue_capacity(int *used, int *capacity) {
 // src/hclib.c:475-480: function and argument of the running task (the
 // root task's when called from the hclib_launch entrypoint)
 void hclib_get_curr_task_info(void (**fp_out)(void *), void **args_out) {
-    if (!g_curr_task) die("hclib_get_curr_task_info: no task is running");
-    if (fp_out) *fp_out = g_curr_task->fp;
-    if (args_out) *args_out = g_curr_task->args;
+    hclib_task_t *t = current_task();
+    if (!t) die("hclib_get_curr_task_info: no task is running");
+    if (fp_out) *fp_out = t->_fp;
+    if (args_out) *args_out = t->args;
 }
 
 // src/hclib-runtime.c:1340-1363: run fp(data) on the main context. The host
@@ -937,45 +986,6 @@ void hclib_get_curr_task_info(void (**fp_out)(void *), void **args_out) {
 void hclib_run_on_main_ctx(void (*fp)(void *), void *data) {
     if (!fp) die("hclib_run_on_main_ctx: null function");
     fp(data);
-}
-
-// src/hclib-locality-graph.c:1020-1022, 1056-1100: the master worker's first
-// pop locale and the locale every worker can reach; both are system memory
-hclib_locale_t *hclib_get_master_place(void) { return &rt().host; }
-hclib_locale_t *hclib_get_central_place(void) { return &rt().host; }
-
-// src/hclib-locality-graph.c:1136-1170: nearest locale of one of the types,
-// breadth-first from `locale`; the graph here is host <-> bound GPU
-hclib_locale_t *hclib_get_closest_locale_of_types(hclib_locale_t *locale, int *types, int ntypes) {
-    const int n = hclib_get_num_locales();
-    hclib_locale_t *order[2] = {locale, locale == hclib_get_locale(0) ? hclib_get_locale(1) : hclib_get_locale(0)};
-    for (int k = 0; k < 2 && k < n; ++k)
-        for (int q = 0; q < ntypes; ++q)
-            if (order[k] && order[k]->type == types[q]) return order[k];
-    return nullptr;
-}
-hclib_locale_t *hclib_get_closest_locale_of_type(hclib_locale_t *locale, int type) {
-    return hclib_get_closest_locale_of_types(locale, &type, 1);
-}
-
-// src/hclib-locality-graph.c:917-940: each worker's private (first pop)
-// locale; one worker, the control thread, whose locale is system memory
-hclib_locale_t **hclib_get_thread_private_locales(void) {
-    hclib_locale_t **v = (hclib_locale_t **)malloc(sizeof(hclib_locale_t *));
-    if (!v) die("out of memory");
-    v[0] = &rt().host;
-    return v;
-}
-
-// src/hclib-locality-graph.c:829-837
-void hclib_locale_mark_special(hclib_locale_t *locale, const char *special_type) {
-    if (!locale || !special_type) die("hclib_locale_mark_special: null argument");
-    if (locale->special_type) {
-        if (strcmp(locale->special_type, special_type) != 0)
-            die("hclib_locale_mark_special: locale already marked '%s'", locale->special_type);
-    } else {
-        locale->special_type = special_type;
-    }
 }
 
 // src/hclib.c:16-30 and src/hclib-runtime.c:231-239, 396: loop distribution
@@ -999,11 +1009,14 @@ loop_dist_func hclib_lookup_dist_func(unsigned id) {
     return dist_funcs()[id];
 }
 
-hclib_locale_t *hclib_get_closest_locale(void) { return &rt().host; }
-
+// the GPU locale standing for HIP device `index` (the first one of the graph)
 hclib_locale_t *hclib_hip_gpu_locale(int index) {
-    rt().gpu_index = index;
-    return &rt().gpu;
+    const int n = hclib_get_num_locales();
+    for (int i = 0; i < n; ++i) {
+        hclib_locale_t *l = hclib_get_locale(i);
+        if (hxh::locale_device(l) == index) return l;
+    }
+    die("hclib_hip_gpu_locale: the locality graph has no locale for GPU %d", index);
 }
 
 void hclib_hip_register_async_kind(generic_frame_ptr fp, int kind) {

@@ -169,6 +169,10 @@ inline void launch(const int nworkers, const char **deps, int ndeps, T &&lambda)
 }
 
 inline int get_current_worker() { return hclib_get_current_worker(); }
+// inc/hclib_cpp.h:49-58 (src/hclib_cpp.cpp)
+inline hclib_worker_state *current_ws() { return ::current_ws(); }
+inline locale_t **get_thread_private_locales() { return hclib_get_thread_private_locales(); }
+inline locale_t *get_master_place() { return hclib_get_master_place(); }
 inline int get_num_workers() { return hclib_get_num_workers(); }
 inline locale_t *get_closest_locale() { return hclib_get_closest_locale(); }
 // inc/hclib_cpp.h:53-57
