@@ -57,16 +57,31 @@ def wide_tree(H, rank, world, be, steps=2, split=7):
     H.uts(T1XL, rank, world, split) if world > 1 else H.uts(T1XL)
     dist.barrier(world, be)
     t0 = time.perf_counter()
+    kms = 0.0
     for _ in range(steps):
         r = H.uts(T1XL, rank, world, split) if world > 1 else H.uts(T1XL)
+        kms += r["kernel_ms"] / steps
     dist.barrier(world, be)
     el = dist.max_over_ranks(time.perf_counter() - t0, world, be)
     tot = dist.combine_counts(r["nodes"], r["leaves"], r["max_depth"], world, be)
     if tot != T1XL_GOLD:
         raise SystemExit(f"T1XL mismatch: {tot} != {T1XL_GOLD}")
-    return {"workload": f"test/uts T1XL ({T1XL}) sharded over {world} GPU(s), split depth {split}",
-            "nodes_per_s": T1XL_GOLD[0] * steps / el, "ms_per_step": el * 1e3 / steps,
-            "scaling": "strong", "bit_exact": True}
+    per_rank = dist.gather_floats(kms, world, be)
+    nodes = dist.gather_floats(float(r["nodes"]), world, be)
+    out = {"workload": f"test/uts T1XL ({T1XL}) sharded over {world} GPU(s), split depth {split}",
+           "nodes_per_s": T1XL_GOLD[0] * steps / el, "ms_per_step": el * 1e3 / steps,
+           "scaling": "strong", "bit_exact": True, "kernel_ms_per_rank": per_rank,
+           "nodes_per_rank": [int(n) for n in nodes]}
+    if world > 1:
+        # the same tree searched whole by each GPU alone (outside the timed
+        # region): T(1) for the efficiency T(1) / (N * T(N))
+        dist.barrier(world, be)
+        t1 = time.perf_counter()
+        H.uts(T1XL)
+        one = dist.max_over_ranks(time.perf_counter() - t1, world, be)
+        out["ms_one_gpu"] = one * 1e3
+        out["efficiency"] = one / (world * el / steps)
+    return out
 
 
 def measure_triad(H, reps=20, n=1 << 28, sync=None):
@@ -302,6 +317,15 @@ def main():
     if tot != T3L_GOLD:
         raise SystemExit(f"T3L mismatch: {tot} != {T3L_GOLD}")
     value = T3L_GOLD[0] * args.steps / elapsed
+    per_rank_ms = dist.gather_floats(sum(kernel_ms) / len(kernel_ms), world, be)
+    per_rank_nodes = dist.gather_floats(float(last["nodes"]), world, be)
+    t3l_one = None
+    if world > 1:
+        # T(1): the whole tree on each GPU alone, outside the timed region
+        dist.barrier(world, be)
+        t1 = time.perf_counter()
+        H.uts(T3L)
+        t3l_one = dist.max_over_ranks(time.perf_counter() - t1, world, be)
     wide = None if args.no_extras else wide_tree(H, rank, world, be)
     shard_tri = None
     if world > 1 and not args.no_extras:
@@ -340,8 +364,16 @@ def main():
             "bit_exact": True,
             "uts_kernel_ms_rank0": sum(kernel_ms) / len(kernel_ms),
             "parallelism": f"shard{world} (hash-partitioned frontier, RCCL all-reduce of counts)",
+            "bound": "span: 17,844 dependent SHA-1 levels; no partition can shorten the critical path, "
+                     "so strong-scaling efficiency on T3L tends to 1/N (DESIGN.md §6)",
         },
+        "collectives": dist.describe(world, be),
+        "kernel_ms_per_rank": per_rank_ms,
+        "nodes_per_rank": [int(n) for n in per_rank_nodes],
     }
+    if t3l_one is not None:
+        out["ms_one_gpu"] = t3l_one * 1e3
+        out["efficiency"] = t3l_one / (world * elapsed / args.steps)
     if wide:
         out["wide_tree"] = wide
     if shard_tri:

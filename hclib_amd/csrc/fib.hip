@@ -2,41 +2,30 @@
 //
 // Each fib(n) call is one task (one lane-item), exactly as each
 // hclib_async(fib, ...) is one task in the reference (fib.c:57-71). A task
-// with n >= 2 opens a finish scope: a join record whose counter starts at 2
-// (the two child asyncs; the reference's finish counter is the owner's 1 +
-// the two check-ins, src/hclib-runtime.c:1219-1247, 431-446). Children add
-// their result and check out with ONE 64-bit atomic: word = count<<56 | sum.
-// The child that brings the count to zero runs the continuation
-// (res = lhs + rhs, fib.c:70) inline and checks out of the parent scope —
+// with n >= 2 opens a finish scope for its two child asyncs (the reference's
+// finish counter is the owner's 1 + the two check-ins, src/hclib-runtime.c:
+// 1219-1247, 431-446) with the generic device finish of hx_finish.h: the
+// children add their result and check out with ONE 64-bit atomic, and the
+// child that closes the scope runs the continuation (res = lhs + rhs,
+// fib.c:70: the scope's sum) inline and checks out of the parent scope —
 // the GPU analogue of help_finish's work-shift (no stacks, no fibers). This
-// also is the DDT form (fib.c:113-141): the join word is the promise pair
+// also is the DDT form (fib.c:113-141): the scope word is the promise pair
 // subres[0..1] and the last put releases fib_ddt_res.
 #include <string.h>
 
 #include "hx_module.h"
+#include "../../include/hclib_hip/hx_finish.h"
 
 namespace hx {
 
-constexpr uint32_t kFibRoot = 0xffffffffu;
-constexpr unsigned long long kOne = 1ull << 56;
-constexpr unsigned long long kSumMask = kOne - 1;
-
-struct alignas(16) FibJoin {
-    unsigned long long word;  // count << 56 | partial sum
-    uint32_t parent;          // join index of the enclosing scope, or kFibRoot
-    uint32_t pad;
-};
-
 struct FibCtx {
     int n;
-    FibJoin *joins;
-    uint32_t *join_next;  // bump allocator (one atomic per wave batch)
-    uint32_t join_cap;
-    unsigned long long *result;
+    FinishArena fin;
 };
 
 struct FibKind {
-    // template = the scope {n, join}; child k is fib(n-1-k)
+    // template = {n + 1 of the parent call, the parent's scope}; child k is
+    // fib(n - 1 - k) of that call
     static constexpr int kTmplWords = 2;
     static constexpr int kWords = 4;
     static constexpr bool kPure = false;           // scopes are opened / checked out in HBM
@@ -55,21 +44,8 @@ struct FibKind {
 
     __device__ static int roots(const Ctx &c, Acc &, uint32_t *tmpl) {
         tmpl[0] = (uint32_t)c.n + 1;  // child 0 of {n+1, root} is fib(n)
-        tmpl[1] = kFibRoot;
+        tmpl[1] = kScopeRoot;
         return 1;
-    }
-
-    // check out of scope j with value v; run continuations while last
-    __device__ static void check_out(const Ctx &c, Acc &acc, uint32_t j, unsigned long long v) {
-        while (j != kFibRoot) {
-            FibJoin *J = &c.joins[j];
-            const unsigned long long old = add_agent(&J->word, v - kOne);
-            if ((old >> 56) != 1) return;  // sibling still running
-            v += old & kSumMask;           // res = lhs + rhs (fib.c:70)
-            acc.joins += 1;
-            j = ld_agent(&J->parent);
-        }
-        st_agent(c.result, v);
     }
 
     __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
@@ -77,26 +53,14 @@ struct FibKind {
         acc.tasks += 1;
         const int n = (int)t[0] - 1 - (int)k;
         const bool spawn = n >= 2;
-        // one bump allocation per wave for every lane that opens a scope
-        const unsigned long long m = __ballot(spawn);
-        uint32_t base = 0;
-        if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            if (lane_id() == leader) base = add_agent(c.join_next, (uint32_t)__popcll(m));
-            base = __shfl(base, leader, 64);
-        }
-        if (!spawn) {
-            check_out(c, acc, t[1], (unsigned long long)n);
+        // FINISH { async fib(n-1); async fib(n-2); }  (one bump allocation
+        // per wave for every lane that opens a scope)
+        const uint32_t j = finish_open(c.fin, spawn, t[1], 2, 0, err);
+        if (!spawn) {  // a leaf returns n: check out, continuations inline
+            acc.joins += finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
             return 0;
         }
-        const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
-        if (j >= c.join_cap) {
-            dev_error(err, kErrArena);
-            return 0;
-        }
-        FibJoin *J = &c.joins[j];
-        st_agent(&J->word, 2ull << 56);
-        st_agent(&J->parent, t[1]);
+        if (j == kScopeRoot) return 0;  // arena error (reported)
         child[0] = (uint32_t)n;  // children fib(n-1), fib(n-2)
         child[1] = j;
         return 2;
@@ -134,16 +98,16 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
         set_error("hclib_hip_fib: n too large for the join arena");
         return HCLIB_HIP_EINVAL;
     }
-    const size_t jb = sizeof(FibJoin) * (size_t)(scopes + 1);
+    const size_t jb = sizeof(FinishScope) * (size_t)(scopes + 1);
     void *dmem = nullptr;
     HX_HIP(hipMalloc(&dmem, jb + 512));
     FibCtx ctx;
     ctx.n = n;
-    ctx.joins = (FibJoin *)dmem;
-    ctx.join_next = (uint32_t *)((char *)dmem + ((jb + 255) & ~(size_t)255));
-    ctx.join_cap = (uint32_t)(scopes + 1);
-    ctx.result = (unsigned long long *)(ctx.join_next + 16);
-    HX_HIP(hipMemsetAsync(ctx.join_next, 0, 256, m.stream));
+    ctx.fin.scopes = (FinishScope *)dmem;
+    ctx.fin.next = (uint32_t *)((char *)dmem + ((jb + 255) & ~(size_t)255));
+    ctx.fin.cap = (uint32_t)(scopes + 1);
+    ctx.fin.root_value = (unsigned long long *)(ctx.fin.next + 16);
+    HX_HIP(hipMemsetAsync(ctx.fin.next, 0, 256, m.stream));
     PoolView pool;
     HX_TRY(make_pool((uint32_t)env_int("HCLIB_HIP_DEQUES", 64),
                      (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
@@ -167,7 +131,7 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     SchedGlobals gl;
     int rc = finish_sched(&gl, "hclib_hip_fib");
     unsigned long long v = 0;
-    if (rc == HCLIB_HIP_OK) rc = hip_check(hipMemcpy(&v, ctx.result, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc == HCLIB_HIP_OK) rc = hip_check(hipMemcpy(&v, ctx.fin.root_value, 8, hipMemcpyDeviceToHost), "hipMemcpy");
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
     (void)hipFree(dmem);

@@ -70,6 +70,7 @@ struct Runtime {
     unsigned long long spawned = 0, future_waits = 0, end_finishes_nb = 0, yields = 0, yield_iters = 0;
     unsigned long long device_items = 0, device_batches = 0, device_chunks_pushed = 0, device_chunks_stolen = 0;
     double device_ms = 0;
+    std::vector<hclib_hip_wave_stats_t> waves;  // per device wave, summed over launches
 };
 
 Runtime &rt() {
@@ -154,6 +155,21 @@ void add_sched_counters(Runtime &R) {
     R.device_batches += c[13];
     R.device_chunks_pushed += c[14];
     R.device_chunks_stolen += c[15];
+    const int n = hclib_hip_last_wave_stats(nullptr, 0);
+    std::vector<hclib_hip_wave_stats_t> w((size_t)n);
+    hclib_hip_last_wave_stats(w.data(), n);
+    if (R.waves.size() < w.size()) R.waves.resize(w.size(), hclib_hip_wave_stats_t{});
+    for (size_t i = 0; i < w.size(); ++i) {
+        hclib_hip_wave_stats_t &a = R.waves[i];
+        a.executed += w[i].executed;
+        a.spawned += w[i].spawned;
+        a.batches += w[i].batches;
+        a.chunks_pushed += w[i].chunks_pushed;
+        a.chunks_stolen += w[i].chunks_stolen;
+        a.items_stolen += w[i].items_stolen;
+        a.xcd = w[i].xcd;
+        for (int x = 0; x < 8; ++x) a.stolen_from[x] += w[i].stolen_from[x];
+    }
 }
 
 int kind_of(generic_frame_ptr fp) {
@@ -1031,30 +1047,43 @@ void hclib_hip_register_forasync_body(void *fct, int body) {
     rt().bodies[fct] = body;
 }
 
-// hclib_print_runtime_stats, src/hclib-runtime.c:1370-1410
+// hclib_print_runtime_stats, src/hclib-runtime.c:1370-1410: the reference's
+// report layout, one line per worker, then the totals. Worker 0 is the host
+// control thread. The device's workers are the megakernel's waves: one line
+// per wave of the device launches so far (its own record, summed over
+// launches: tasks run, children created, chunks taken from other deques
+// and the tasks in them, and from which XCD's deques they came).
 void hclib_print_runtime_stats(FILE *fp) {
-    // the layout of the reference's HCLIB_STATS report (src/hclib-runtime.c:
-    // 1370-1410): one line per worker, then the totals. Worker 0 is the host
-    // control thread; the device's waves are reported as one line of their
-    // batches and chunk deque traffic (steals = chunks taken from a deque
-    // other than the wave's home deque).
     Runtime &R = rt();
     fprintf(fp, "===== HClib statistics: =====\n");
     fprintf(fp,
             "  Worker 0: %llu tasks executed, %llu tasks spawned, %llu tasks scheduled, 0 steals, "
             "0 stolen tasks, 0.000000 tasks per steal, stolen from = [ 0 ]\n",
             R.host_tasks + R.device_tasks, R.spawned, R.spawned);
+    unsigned long long dev_exec = 0;
+    for (size_t i = 0; i < R.waves.size(); ++i) {
+        const hclib_hip_wave_stats_t &w = R.waves[i];
+        dev_exec += w.executed;
+        fprintf(fp,
+                "  Device wave %zu (XCD %llu): %llu tasks executed, %llu tasks spawned, %llu batches, "
+                "%llu chunks pushed, %llu steals, %llu stolen tasks, %f tasks per steal, stolen from = [ ",
+                i, (unsigned long long)w.xcd, (unsigned long long)w.executed, (unsigned long long)w.spawned,
+                (unsigned long long)w.batches, (unsigned long long)w.chunks_pushed,
+                (unsigned long long)w.chunks_stolen, (unsigned long long)w.items_stolen,
+                w.chunks_stolen ? (double)w.items_stolen / (double)w.chunks_stolen : 0.0);
+        for (int x = 0; x < 8; ++x) fprintf(fp, "%llu ", (unsigned long long)w.stolen_from[x]);
+        fprintf(fp, "]\n");
+    }
     if (R.device_tasks)
         fprintf(fp,
-                "  Device (%d waves): %llu device items executed in %llu batches, %llu chunks pushed, "
+                "  Device (%zu waves): %llu device items executed in %llu batches, %llu chunks pushed, "
                 "%llu chunks stolen, %f items per batch, %.3f ms\n",
-                hclib_hip_num_workers(), R.device_items, R.device_batches, R.device_chunks_pushed,
-                R.device_chunks_stolen,
+                R.waves.size(), R.device_items, R.device_batches, R.device_chunks_pushed, R.device_chunks_stolen,
                 R.device_batches ? (double)R.device_items / (double)R.device_batches : 0.0, R.device_ms);
     fprintf(fp,
             "Total: %llu tasks, %llu end finishes, %llu future waits, %llu non-blocking end finishes, "
             "0 ctx creates, %llu yields, %f iters per yield on average\n",
-            R.host_tasks + R.device_tasks + R.device_items, R.end_finishes, R.future_waits, R.end_finishes_nb,
+            R.host_tasks + R.device_tasks + dev_exec, R.end_finishes, R.future_waits, R.end_finishes_nb,
             R.yields, R.yields ? (double)R.yield_iters / (double)R.yields : 0.0);
 }
 

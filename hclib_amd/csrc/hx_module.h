@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/hclib_hip.h"
 #include "../../include/hclib_hip/hx_sched.h"
@@ -25,6 +26,10 @@ struct Module {
     size_t pool_bytes = 0;
     SchedGlobals *globals = nullptr;
     unsigned long long last_counters[16] = {};  // counters of the last megakernel launch
+    // per-wave records of megakernel launches (WaveStat, hx_sched.h)
+    WaveStat *wave_stats = nullptr;
+    uint32_t wave_stats_cap = 0;
+    std::vector<WaveStat> last_waves;  // the last launch's, copied back by finish_sched
 };
 
 Module &mod();

@@ -87,6 +87,8 @@ int reset_sched(const PoolView &pool, uint32_t outstanding_init) {
     SchedGlobals init;
     memset(&init, 0, sizeof(init));
     init.outstanding = outstanding_init;
+    init.wave_stats = m.wave_stats;
+    init.wave_stats_cap = m.wave_stats_cap;
     HX_HIP(hipMemcpyAsync(m.globals, &init, sizeof(init), hipMemcpyHostToDevice, m.stream));
     return HCLIB_HIP_OK;
 }
@@ -107,8 +109,14 @@ int finish_sched(SchedGlobals *host_copy, const char *who) {
     Module &m = g_mod;
     HX_HIP(hipMemcpyAsync(host_copy, m.globals, sizeof(SchedGlobals), hipMemcpyDeviceToHost,
                           m.stream));
+    const uint32_t nw_cap = m.wave_stats_cap;
     HX_HIP(hipStreamSynchronize(m.stream));
     memcpy(m.last_counters, host_copy->counters, sizeof(m.last_counters));
+    // every wave of the grid leaves exactly once: counters[kCtrWaves] records
+    uint64_t nw = host_copy->counters[kCtrWaves];
+    if (nw > nw_cap) nw = nw_cap;
+    m.last_waves.resize(nw);
+    if (nw) HX_HIP(hipMemcpy(m.last_waves.data(), m.wave_stats, nw * sizeof(WaveStat), hipMemcpyDeviceToHost));
     if (host_copy->err) {
         set_error("%s: device error %u (%s)", who, host_copy->err, err_name(host_copy->err));
         return HCLIB_HIP_EDEVICE;
@@ -153,6 +161,8 @@ int hclib_hip_init(int device) {
     HX_HIP(hipEventCreate(&m.ev0));
     HX_HIP(hipEventCreate(&m.ev1));
     HX_HIP(hipMalloc((void **)&m.globals, sizeof(SchedGlobals)));
+    m.wave_stats_cap = (uint32_t)m.num_cus * 32;  // 32 waves per CU at most
+    HX_HIP(hipMalloc((void **)&m.wave_stats, sizeof(WaveStat) * m.wave_stats_cap));
     m.inited = true;
     return HCLIB_HIP_OK;
 }
@@ -163,6 +173,7 @@ void hclib_hip_finalize(void) {
     (void)hipStreamSynchronize(m.stream);
     if (m.pool_mem) (void)hipFree(m.pool_mem);
     (void)hipFree(m.globals);
+    (void)hipFree(m.wave_stats);
     (void)hipEventDestroy(m.ev0);
     (void)hipEventDestroy(m.ev1);
     (void)hipStreamDestroy(m.stream);
@@ -173,6 +184,13 @@ int hclib_hip_num_cus(void) { return g_mod.inited ? g_mod.num_cus : 0; }
 
 void hclib_hip_last_sched_counters(uint64_t out[16]) {
     for (int i = 0; i < 16; ++i) out[i] = g_mod.last_counters[i];
+}
+
+int hclib_hip_last_wave_stats(hclib_hip_wave_stats_t *out, int max) {
+    static_assert(sizeof(hclib_hip_wave_stats_t) == sizeof(WaveStat), "layout");
+    const int n = (int)g_mod.last_waves.size();
+    for (int i = 0; out && i < n && i < max; ++i) memcpy(&out[i], &g_mod.last_waves[(size_t)i], sizeof(WaveStat));
+    return n;
 }
 
 int hclib_hip_sched_begin(uint32_t entry_words, uint32_t chunk, int waves_per_cu,

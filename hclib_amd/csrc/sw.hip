@@ -665,6 +665,9 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     // rows: one wave per CU owns tile rows (all resident, so every wait ends)
     int wpc = env_int("HCLIB_HIP_SW_WAVES_PER_CU", rows ? 1 : 2);
     if (wpc > per_cu) wpc = per_cu;
+    // the generic promise DAG launches at most 8 waves per CU
+    // (hclib_hip_dag_begin); clamp here rather than fail its argument check
+    if (dag && wpc > 8) wpc = 8;
     if (wpc < 1) wpc = 1;
     int grid = m.num_cus * wpc;
     if (rows && grid > (int)nth) grid = (int)nth;

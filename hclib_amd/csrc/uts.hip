@@ -134,6 +134,8 @@ struct UtsCtx {
     int lds_tables;  // rules/thr fit the per-wave LDS cache
     uint32_t bin_thr;  // BIN trees: a node has m children iff rand < bin_thr (every depth >= 1)
     int nthr;        // words in thr
+    int geo_depth;   // kUtsGeoFixed: depths 1..geo_depth-1 use table 0, deeper nodes are leaves
+    uint32_t thr16[16];  // kUtsGeoFixed: thresholds 1..16 of table 0 (kernel arguments: SGPRs)
     const int4 *rules;
     const uint32_t *thr;
     unsigned long long *hist;
@@ -153,11 +155,34 @@ enum UtsMode : int {
     kUtsRulesGlobal = 0,  // depth rules in device memory (large tables)
     kUtsRulesLds = 1,     // depth rules cached in LDS
     kUtsBin = 2,          // BIN tree: one rule for every depth >= 1 (no lookup at all)
+    kUtsGeoFixed = 3,     // GEO tree with one table above a depth and leaves below
+                          // (shape -a 3: T1, T1L, T1XL): no rule lookup, the first 16
+                          // thresholds in registers, the rest (P(n > 16) = 0.8^17 at
+                          // b = 4) binary-searched in LDS
 };
 
 template <int MODE>
 __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32_t *err) {
     if (MODE == kUtsBin) return r < c.bin_thr ? c.m : 0;
+    if (MODE == kUtsGeoFixed) {
+        if (d >= c.geo_depth) return 0;
+        int n = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) n += c.thr16[k] <= r ? 1 : 0;
+        if (n == 16) {  // rare: thresholds 17..100 (table 0 in LDS)
+            int lo = 16, hi = 100;
+#pragma unroll
+            for (int s = 0; s < 7; ++s) {
+                int mid = (lo + hi + 1) >> 1;
+                if (lo < hi) {
+                    if (s_thr[mid] <= r) lo = mid;
+                    else hi = mid - 1;
+                }
+            }
+            n = lo;
+        }
+        return n;
+    }
     constexpr bool LDS = MODE == kUtsRulesLds;
     int ri = d;
     if (d >= c.nrules) {
@@ -189,6 +214,10 @@ template <int MODE, int FEAT>
 struct UtsKind {
     // template = the node {state[5], height}; an item = its children [k, kend)
     static constexpr int kTmplWords = 6;
+    // BIN trees spawn m <= 8 children: 8 pieces keep every batch uniform (the
+    // register carry); GEO trees take 5 pieces so their ring fits 512 items
+    // (16 KiB) and twice the waves stay resident per CU
+    static constexpr int kPieces = MODE == kUtsBin ? 8 : 5;
     static constexpr int kWords = 8;
     static constexpr bool kPure = FEAT == 0;  // the histogram's atomics are side effects
     static constexpr bool kBoundedChildren = true;  // <= 100 (the root goes through roots())
@@ -251,12 +280,20 @@ struct UtsKind {
     }
 };
 
-constexpr int kUtsCap = 1024;  // ring items per wave (32 KiB of LDS)
+// ring items per wave: 1024 (32 KiB of LDS) for BIN trees, 512 (16 KiB) for
+// the others (5 pieces per task: one batch pushes at most 64 * 7 items)
+template <int MODE>
+constexpr int uts_cap() { return MODE == kUtsBin ? 1024 : 512; }
 
 template <int MODE, int FEAT>
 __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, SchedGlobals *g,
                                                    SchedConfig cfg) {
+    constexpr int kUtsCap = uts_cap<MODE>();
     __shared__ WaveStack<UtsKind<MODE, FEAT>, kUtsCap> st;
+    if (MODE == kUtsGeoFixed) {
+        for (int i = threadIdx.x; i < 128; i += 64) s_thr[i] = ctx.thr[i];
+        __syncthreads();
+    }
     if (MODE == kUtsRulesLds) {
         // the per-node rule lookup becomes LDS-latency (no dependent HBM/L2 loads)
         for (int i = threadIdx.x; i < ctx.nrules; i += 64) s_rules[i] = ctx.rules[i];
@@ -519,6 +556,18 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     ctx.lds_tables = (T.rules.size() <= kUtsLdsRules && T.thr.size() <= kUtsLdsThr) ? 1 : 0;
     ctx.bin_thr = 0;
     ctx.nthr = (int)T.thr.size();
+    // one GEO table for depths 1..D-1, constant 0 children from D on
+    int geo_depth = 0;
+    {
+        const int nr = (int)T.rules.size();
+        int d = 1;
+        while (d < nr && T.rules[d].x == 2 && T.rules[d].z == 0) ++d;
+        bool rest_zero = d > 1 && T.stationary;
+        for (int e = d; e < nr && rest_zero; ++e) rest_zero = T.rules[e].x == 0 && T.rules[e].y == 0;
+        if (rest_zero && T.thr.size() >= 128) geo_depth = d;
+    }
+    ctx.geo_depth = geo_depth;
+    for (int k = 0; k < 16; ++k) ctx.thr16[k] = geo_depth ? T.thr[1 + k] : 0u;
 
     PoolView pool;
     const uint32_t nq = (uint32_t)env_int("HCLIB_HIP_DEQUES", 64);
@@ -527,9 +576,10 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // span-bound BIN trees run fastest with 2 waves per CU (fewer idle pollers,
     // fewer hand-offs); throughput-bound GEO trees with 4
     const bool bin = params->type == 0 && T.rules.size() == 2 && T.rules[1].x == 1 && T.stationary;
+    const bool geo_fixed = !bin && geo_depth > 0 && env_int("HCLIB_HIP_UTS_GEO_FIXED", 1);
     const int grid = env_int("HCLIB_HIP_GRID", 0) > 0
                          ? env_int("HCLIB_HIP_GRID", 0)
-                         : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", bin ? 2 : 4);
+                         : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", bin ? 2 : 8);
     SchedConfig cfg;
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_SPILL_HI", 512);
     cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", 96);
@@ -544,12 +594,13 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     const bool feat = nshards > 1 || max_levels > 0;
     if (bin) ctx.bin_thr = (uint32_t)T.rules[1].y;
-    const int mode = bin ? kUtsBin : (ctx.lds_tables ? kUtsRulesLds : kUtsRulesGlobal);
+    const int mode = bin ? kUtsBin : geo_fixed ? kUtsGeoFixed : (ctx.lds_tables ? kUtsRulesLds : kUtsRulesGlobal);
     typedef void (*uts_kernel_t)(UtsCtx, PoolView, SchedGlobals *, SchedConfig);
-    static const uts_kernel_t kernels[3][2] = {
+    static const uts_kernel_t kernels[4][2] = {
         {k_uts_search<kUtsRulesGlobal, 0>, k_uts_search<kUtsRulesGlobal, 1>},
         {k_uts_search<kUtsRulesLds, 0>, k_uts_search<kUtsRulesLds, 1>},
         {k_uts_search<kUtsBin, 0>, k_uts_search<kUtsBin, 1>},
+        {k_uts_search<kUtsGeoFixed, 0>, k_uts_search<kUtsGeoFixed, 1>},
     };
     hipLaunchKernelGGL(kernels[mode][feat ? 1 : 0], dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
     HX_HIP(hipGetLastError());

@@ -75,6 +75,30 @@ def max_over_ranks(x: float, world: int, backend: str = "nccl") -> float:
     return float(t[0])
 
 
+def gather_floats(x: float, world: int, backend: str = "nccl"):
+    """Every rank's value of x, in rank order (all_gather)."""
+    if world == 1:
+        return [float(x)]
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=_device(backend))
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(o[0]) for o in out]
+
+
+def describe(world: int, backend: str) -> dict:
+    """What the collective layer is: world size and backend as the process
+    group reports them (RCCL is torch's "nccl" backend on ROCm)."""
+    if world == 1:
+        return {"world_size": 1, "backend": None}
+    import torch.distributed as dist
+
+    be = dist.get_backend()
+    return {"world_size": dist.get_world_size(), "backend": "rccl" if be == "nccl" else be}
+
+
 def barrier(world: int, backend: str = "nccl") -> None:
     import torch
 
@@ -144,7 +168,8 @@ class _HipBand:
         from . import SwBand
 
         self.band = SwBand(s1, s2, tw, th, j0, j1)
-        self.stream = torch.cuda.current_stream().cuda_stream
+        self.torch_stream = torch.cuda.current_stream()
+        self.stream = self.torch_stream.cuda_stream
 
     def rows(self, i0, i1, left, right):
         self.band.rows(i0, i1, None if left is None else left.data_ptr(),
@@ -200,16 +225,24 @@ class ShardedSw:
             dist.send(t.cpu(), dst=self.rank + 1, group=self.group)
 
     def run(self):
+        import contextlib
+
         import torch
 
         th = self.th
-        for i0, i1 in self.blocks:
-            if self.left is not None:
-                self._recv(self.left[i0 * th:i1 * th])
-            self.band.rows(i0, i1, self.left, self.right)
-            if self.right is not None:
-                self._send(self.right[i0 * th:i1 * th])
-        corner, tiles = self.band.end()
+        # the received column's copy, the band launch and the send's read all
+        # run on the stream the band was built on, whatever stream is current
+        # when run() is called
+        ts = getattr(self.band, "torch_stream", None)
+        ctx = torch.cuda.stream(ts) if ts is not None else contextlib.nullcontext()
+        with ctx:
+            for i0, i1 in self.blocks:
+                if self.left is not None:
+                    self._recv(self.left[i0 * th:i1 * th])
+                self.band.rows(i0, i1, self.left, self.right)
+                if self.right is not None:
+                    self._send(self.right[i0 * th:i1 * th])
+            corner, tiles = self.band.end()
         if self.world == 1:
             return corner, tiles
         import torch.distributed as dist

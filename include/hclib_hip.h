@@ -70,6 +70,24 @@ const char *hclib_hip_version(void);
  * [12] waves, [13] batches, [14] chunks pushed, [15] chunks stolen. */
 void hclib_hip_last_sched_counters(uint64_t out[16]);
 
+/* Per-wave records of the last megakernel launch (the per-worker lines of
+ * HCLIB_STATS, src/hclib-runtime.c:1370-1410): each wave writes its own
+ * record as it leaves. Summed over the waves, batches / chunks_pushed /
+ * chunks_stolen equal hclib_hip_last_sched_counters [13] / [14] / [15].
+ * Copies at most `max` records to out; returns the number of waves. */
+typedef struct {
+    uint64_t executed;      /* tasks run (one lane of a batch each) */
+    uint64_t spawned;       /* children created */
+    uint64_t batches;
+    uint64_t chunks_pushed; /* chunks given to the HBM deques */
+    uint64_t chunks_stolen; /* chunks taken from a deque other than the wave's home deque */
+    uint64_t items_stolen;  /* tasks in those chunks */
+    uint64_t xcd;           /* the XCD the wave ran on */
+    uint64_t reserved;
+    uint64_t stolen_from[8]; /* chunks taken from each XCD's deques */
+} hclib_hip_wave_stats_t;
+int hclib_hip_last_wave_stats(hclib_hip_wave_stats_t *out, int max);
+
 /* L2 atomic-throughput calibration: the saturated rate (million atomic
  * ops per second, whole GPU) of one access shape the runtime's atomics use,
  * the "peak" fib/SW/scheduler atomic rates are priced against.

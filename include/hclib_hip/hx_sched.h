@@ -58,6 +58,20 @@ struct alignas(256) QueueHdr {
     uint32_t pad1[31];
 };
 
+// One wave's scheduler statistics, written by the wave itself when it
+// leaves the megakernel (the HCLIB_STATS per-worker record of
+// src/hclib-runtime.c:83-104 with the device's vocabulary): items executed
+// (one lane of a batch = one task run), tasks spawned (children created),
+// batches, chunks it pushed to / took from the HBM deques, the items in the
+// chunks it took, and which XCD's deques those chunks came from.
+struct WaveStat {
+    unsigned long long executed, spawned, batches, chunks_pushed, chunks_stolen, items_stolen;
+    unsigned long long xcd;                 // XCD the wave ran on
+    unsigned long long reserved;
+    unsigned long long stolen_from[8];      // chunks taken from each XCD's deques
+};
+static_assert(sizeof(WaveStat) == 128, "WaveStat is 16 words");
+
 // Global scheduler state shared by all waves of one launch (device memory).
 struct alignas(256) SchedGlobals {
     uint32_t outstanding;  // chunks queued + waves holding work
@@ -68,6 +82,8 @@ struct alignas(256) SchedGlobals {
     uint32_t pad2[63];
     unsigned long long counters[16];  // [0..7] kind-specific, [8..15] scheduler
     unsigned long long maxes[4];      // kind-specific reductions (atomic max)
+    WaveStat *wave_stats;             // per-wave records (indexed by blockIdx.x), or null
+    uint32_t wave_stats_cap;          // records available
 };
 
 // Diagnostic build (-DHX_STAMPS=1): per-phase s_memtime stamps, enabled at run
@@ -133,8 +149,23 @@ struct SchedConfig {
 //                                     // results are dropped)
 //   static constexpr bool kBoundedChildren;  // process() never returns >= kMaxChildren
 
-constexpr int kPieces = 8;                // range items one task's children are pushed as
-constexpr int kGroupMax = kPieces + 2;    // items one lane pushes per batch (2 residual pieces)
+// Range items one task's children are pushed as (Kind::kPieces, default 8):
+// a task with c children becomes min(c, pieces) items. Fewer pieces need a
+// smaller ring (one batch pushes at most 64 * (pieces + 2) items), so a
+// kind with wide nodes can trade residual splitting for LDS, i.e. for more
+// resident waves per CU.
+template <class K, class = void>
+struct KindPieces {
+    static constexpr int value = 8;
+};
+template <class K>
+struct KindPieces<K, decltype((void)K::kPieces)> {
+    static constexpr int value = K::kPieces;
+};
+template <class K>
+constexpr int pieces_of() { return KindPieces<K>::value; }
+template <class K>
+constexpr int group_max_of() { return KindPieces<K>::value + 2; }  // items one lane pushes per batch
 constexpr uint32_t kMaxChildren = 1u << 24;  // kend shares its descriptor word with delta
 
 template <class Kind, int CAP>
@@ -146,6 +177,7 @@ struct WaveStack {
     uint4 t0[TW == 6 ? CAP : 1];   // template words 0..3 (6-word templates)
     uint2 t1[CAP];                 // template words 4..5 (or 0..1)
     uint32_t mark[64];             // tagged group-start marks of the transposed push
+    uint32_t stolen_from[8];       // chunks this wave took from each XCD's deques
 };
 
 template <class Kind, int CAP>
@@ -342,6 +374,14 @@ __device__ __forceinline__ uint32_t xorshift(uint32_t &s) {
     return s;
 }
 
+// ceil(2^16 / mu) for 1 <= mu <= 8 as a scalar select chain (a division
+// would cost a float reciprocal round trip through a VGPR on the batch's
+// critical path); (o * rcp16(mu)) >> 16 == o / mu for o < 1024
+__device__ __forceinline__ uint32_t rcp16(uint32_t mu) {
+    return mu <= 4 ? (mu <= 2 ? (mu == 1 ? 65536u : 32768u) : (mu == 3 ? 21846u : 16384u))
+                   : (mu <= 6 ? (mu == 5 ? 13108u : 10923u) : (mu == 7 ? 9363u : 8192u));
+}
+
 // Uniform push: no lane has a residual range and every lane that spawned a
 // task spawned exactly `mu` (<= kPieces) children — every BIN-tree batch
 // after the root fan-out, every fib batch. Group starts are then
@@ -355,7 +395,7 @@ __device__ __forceinline__ void push_uniform(WaveStack<Kind, CAP> &st, uint32_t 
                                              const uint32_t *child) {
     constexpr uint32_t M = CAP - 1;
     if (spawned) store_tmpl<Kind, CAP>(st, (base + excl) & M, child);
-    const uint32_t rcp = (65536u + mu - 1) / mu;  // wave-uniform (scalar)
+    const uint32_t rcp = rcp16(mu);  // wave-uniform (scalar)
     for (uint32_t r0 = 0; r0 < tout; r0 += kWaveSize) {
         const uint32_t o = r0 + (uint32_t)lane_id();
         if (o < tout) {
@@ -379,6 +419,7 @@ __device__ __forceinline__ void push_outputs(WaveStack<Kind, CAP> &st, uint32_t 
                                              const uint32_t *child, uint32_t k, uint32_t kend,
                                              uint32_t tag) {
     constexpr uint32_t M = CAP - 1;
+    constexpr int kPieces = pieces_of<Kind>();
     const int lane = lane_id();
     if (__ballot(nres != 0 || ucnt > (uint32_t)kPieces) == 0) {
         if (nch) store_tmpl<Kind, CAP>(st, (base + excl) & M, child);
@@ -423,6 +464,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                            const SchedConfig &cfg, WaveStack<Kind, CAP> &st, bool seed_roots) {
     constexpr int TW = Kind::kTmplWords;
     constexpr uint32_t M = CAP - 1;
+    constexpr int kPieces = pieces_of<Kind>();
+    constexpr int kGroupMax = group_max_of<Kind>();
     // a push never comes within kGroupMax of the ring bottom: a spill may
     // leave the bottom item's template up to kGroupMax-1 slots below `bot`
     constexpr uint32_t kRoom = CAP - kGroupMax;
@@ -443,6 +486,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     unsigned long long cyc_busy = 0, cyc_idle = 0, cyc_spill = 0, cyc_form = 0, cyc_proc = 0, cyc_push = 0;
     uint32_t tag = 1;  // mark tags: 16 per batch
     for (int i = lane; i < kWaveSize; i += kWaveSize) st.mark[i] = 0;
+    if (lane < 8) st.stolen_from[lane] = 0;
+    uint32_t n_exec = 0, n_spawn = 0;          // per lane: tasks run, children created
+    unsigned long long items_stolen = 0;
     // register carry: the previous batch's `carry` outputs, lane o holding
     // item o (template ctmpl, child index ck); they form the front of the
     // next batch instead of round-tripping through the LDS ring
@@ -513,7 +559,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             }
             uint32_t n = dequeue_chunk<Kind, CAP>(pool, q, st, g);
             if (n) {
-                if (q != home) ++nsteal;
+                if (q != home) {
+                    ++nsteal;
+                    items_stolen += n;
+                    if (lane == 0) st.stolen_from[(q / qpx) & 7u] += 1;
+                }
                 bot = 0;
                 top = n;
                 active = true;
@@ -555,9 +605,14 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         ++nbatch;
         // hunger signal: use the value loaded one batch ago (its latency hid
         // behind that whole batch), then issue the load for the next batch
-        // (loaded every cfg.hunger batches; consumed that many batches later)
+        // (loaded every cfg.hunger batches; consumed that many batches later).
+        // Narrow frontier: a batch of carried items only, with an empty ring
+        // and spill_lo above one batch, can neither spill nor be kept from
+        // carrying by hunger, so it neither reads nor waits for the signal:
+        // the span-bound chain of a narrow tree runs carry to carry.
+        const bool narrow = carry > 0 && size == 0 && cfg.spill_lo > (uint32_t)kWaveSize;
         uint32_t outst = cfg.nwaves;
-        if (cfg.hunger) {
+        if (cfg.hunger && !narrow) {
             if (hunger_in == 0) {
                 outst_cur = lane0(outst_pf);
                 if (lane == 0) outst_pf = ld_agent(&g->outstanding);
@@ -580,7 +635,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         int cnt = 0;
         unsigned long long ts0 = 0;
         if (HX_STAMPS && cfg.stamps) ts0 = __builtin_amdgcn_s_memtime();
-        if ((uint32_t)lane < carry) {
+        // a batch of carried items only (take_ring == 0) loads nothing from
+        // the ring: its idle lanes run (pure kinds) on a carried template
+        if ((uint32_t)lane < carry || take_ring == 0) {
 #pragma unroll
             for (int i = 0; i < TW; ++i) tmpl[i] = ctmpl[i];
             k = ck;
@@ -615,6 +672,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         const uint32_t rlen = has ? kend - k - 1u : 0u;
         const uint32_t nres = rlen == 0 ? 0u : (rlen == 1 ? 1u : 2u);
         uint32_t ucnt = cnt > 0 ? (uint32_t)cnt : 0u;
+        n_exec += has ? 1u : 0u;
+        n_spawn += has ? ucnt : 0u;
         if (!Kind::kBoundedChildren && ucnt >= kMaxChildren) {
             dev_error(&g->err, kErrBadTask);
             ucnt = 0;
@@ -651,7 +710,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     (uint32_t)(spawn >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
                 const uint32_t dst = nch != 0 ? rk : nsp + ((uint32_t)lane - rk);
                 const int src_of_rank = __builtin_amdgcn_ds_permute((int)(dst * 4u), lane);
-                const uint32_t rcp = (65536u + mu - 1) / mu;
+                const uint32_t rcp = rcp16(mu);
                 const uint32_t o = (uint32_t)lane;
                 const uint32_t r = (o * rcp) >> 16;  // o / mu (o < 64, mu <= 8)
                 const int src = __builtin_amdgcn_ds_bpermute((int)(r * 4u), src_of_rank);
@@ -734,6 +793,26 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
     }
     acc.flush(g);
+    {
+        // this wave's record (plain stores: the host reads it after the launch)
+        const unsigned long long ex = wave_sum((unsigned long long)n_exec),
+                                 sp = wave_sum((unsigned long long)n_spawn);
+        if (g->wave_stats && gid < g->wave_stats_cap && lane < 16) {
+            unsigned long long v = 0;
+            switch (lane) {
+            case 0: v = ex; break;
+            case 1: v = sp; break;
+            case 2: v = nbatch; break;
+            case 3: v = npush; break;
+            case 4: v = nsteal; break;
+            case 5: v = items_stolen; break;
+            case 6: v = xcc; break;
+            case 7: v = 0; break;
+            default: v = st.stolen_from[lane - 8]; break;
+            }
+            ((unsigned long long *)&g->wave_stats[gid])[lane] = v;
+        }
+    }
     if (lane == 0) {
         add_agent(&g->counters[kCtrBusyCycles], cyc_busy);
         if (HX_STAMPS && cfg.stamps) {

@@ -22,6 +22,11 @@
  *       (include/hclib_hip/hx_dag.h). Blocking, like a finish around the
  *       asyncs; afterwards graph.datum(p) is each promise's value.
  *
+ *   hclib::hip::finish_arena + hx::finish_open / hx::finish_check_out
+ *       nested finish scopes inside device tasks (include/hclib_hip/
+ *       hx_finish.h): the code after a finish is a continuation that the
+ *       last task to leave the scope runs inline.
+ *
  *   hclib::hip::run_tasks<Kind>(ctx, &stats)
  *       a user-defined device task kind on the persistent work-stealing
  *       megakernel (include/hclib_hip/hx_sched.h): the GPU form of
@@ -45,6 +50,7 @@
 #include "hclib_cpp.h"
 #include "hclib_hip.h"
 #include "hclib_hip/hx_dag.h"
+#include "hclib_hip/hx_finish.h"
 #include "hclib_hip/hx_sched.h"
 
 namespace hclib {
@@ -208,6 +214,68 @@ __global__ __launch_bounds__(64) void k_run_tasks(typename Kind::Ctx ctx, hx::Po
     __shared__ hx::WaveStack<Kind, CAP> st;
     hx::run_worker<Kind, CAP>(ctx, pool, g, cfg, st, blockIdx.x == 0);
 }
+
+// Device finish scopes for a task kind (hx_finish.h): `capacity` scopes in
+// device memory plus the bump allocator and the outermost scope's value. A
+// kind keeps view() in its Ctx; tasks open scopes with hx::finish_open and
+// check out with hx::finish_check_out (continuations run inline).
+class finish_arena {
+  public:
+    explicit finish_arena(uint32_t capacity) : cap_(capacity) {
+        const size_t sb = sizeof(hx::FinishScope) * (size_t)capacity;
+        off_ = (sb + 255) & ~(size_t)255;
+        if (hipMalloc(&mem_, off_ + 256) != hipSuccess) mem_ = nullptr;
+        reset();
+    }
+    ~finish_arena() {
+        if (mem_) (void)hipFree(mem_);
+    }
+    finish_arena(const finish_arena &) = delete;
+    finish_arena &operator=(const finish_arena &) = delete;
+    bool ok() const { return mem_ != nullptr; }
+    // every scope free again, no value at the root (ordered on the null stream)
+    void reset() {
+        if (mem_) (void)hipMemset((char *)mem_ + off_, 0, 256);
+    }
+    // pre-open scope ids [0, n) before a launch (e.g. a top-level finish the
+    // root tasks check out of): scope i has counts[i] tasks, parent[i]
+    int preopen(const std::vector<uint32_t> &counts, const std::vector<uint32_t> &parents,
+                const std::vector<uint32_t> &conts) {
+        const size_t n = counts.size();
+        if (n > cap_ || parents.size() != n || conts.size() != n) return HCLIB_HIP_EINVAL;
+        std::vector<hx::FinishScope> h(n);
+        for (size_t i = 0; i < n; ++i) h[i] = hx::FinishScope{(unsigned long long)counts[i] << 56, parents[i], conts[i]};
+        uint32_t next = (uint32_t)n;
+        if (hipMemcpy(mem_, h.data(), n * sizeof(hx::FinishScope), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy((char *)mem_ + off_, &next, 4, hipMemcpyHostToDevice) != hipSuccess)
+            return HCLIB_HIP_EHIP;
+        return HCLIB_HIP_OK;
+    }
+    hx::FinishArena view() const {
+        hx::FinishArena a;
+        a.scopes = (hx::FinishScope *)mem_;
+        a.next = (uint32_t *)((char *)mem_ + off_);
+        a.cap = cap_;
+        a.root_value = (unsigned long long *)((char *)mem_ + off_ + 64);
+        return a;
+    }
+    // the value the outermost scope handed up (after the launch)
+    uint64_t root_value() const {
+        uint64_t v = 0;
+        (void)hipMemcpy(&v, (char *)mem_ + off_ + 64, 8, hipMemcpyDeviceToHost);
+        return v;
+    }
+    uint32_t scopes_opened() const {
+        uint32_t n = 0;
+        (void)hipMemcpy(&n, (char *)mem_ + off_, 4, hipMemcpyDeviceToHost);
+        return n;
+    }
+
+  private:
+    uint32_t cap_;
+    size_t off_ = 0;
+    void *mem_ = nullptr;
+};
 
 struct task_stats {
     uint64_t counters[16];  // [0..7] the kind's Acc::flush counters, [8..15] scheduler

@@ -106,3 +106,35 @@ def test_hclib_stats_report_layout():
     assert "===== HClib statistics: =====" in out
     assert "  Worker 0: " in out and " tasks executed, " in out
     assert "Total: " in out and " end finishes, " in out and " future waits, " in out
+
+
+@pytest.mark.gpu
+def test_hclib_stats_per_wave_device_lines(golden):
+    """HCLIB_STATS=1 after a device UTS task (tests/c/uts_gpu.c, T1): one
+    "Device wave" line per megakernel wave, each written by the wave itself
+    (hclib_hip_last_wave_stats), in the reference's per-worker layout
+    (src/hclib-runtime.c:1370-1410). Their sums equal the launch-wide
+    scheduler counters on the aggregate line, and the tasks they executed
+    are the tree's nodes below the root (the root is counted by roots())."""
+    import re
+
+    g = golden("uts_goldens.json")["published"]["T1"]
+    r = _run(_build("uts_gpu"), *g["args"].split(), env={"HCLIB_STATS": "1"})
+    assert r.returncode == 0, r.stderr
+    pat = re.compile(r"  Device wave (\d+) \(XCD (\d)\): (\d+) tasks executed, (\d+) tasks spawned, "
+                     r"(\d+) batches, (\d+) chunks pushed, (\d+) steals, (\d+) stolen tasks, [\d.]+ tasks per "
+                     r"steal, stolen from = \[ ((?:\d+ ){8})\]")
+    waves = [tuple(int(x) for x in m.groups()[:8]) + (list(map(int, m.group(9).split())),)
+             for m in pat.finditer(r.stdout)]
+    assert len(waves) >= 256 and [w[0] for w in waves] == list(range(len(waves)))
+    agg = re.search(r"  Device \((\d+) waves\): (\d+) device items executed in (\d+) batches, (\d+) chunks "
+                    r"pushed, (\d+) chunks stolen", r.stdout)
+    assert agg, r.stdout[-2000:]
+    nw, items, batches, pushed, stolen = map(int, agg.groups())
+    assert nw == len(waves) and items == g["nodes"]
+    assert sum(w[4] for w in waves) == batches
+    assert sum(w[5] for w in waves) == pushed
+    assert sum(w[6] for w in waves) == stolen
+    assert sum(sum(w[8]) for w in waves) == stolen
+    assert sum(w[2] for w in waves) == g["nodes"] - 1
+    assert len({w[1] for w in waves}) == 8  # waves ran on all eight XCDs

@@ -53,3 +53,23 @@ def test_device_promise_dag_on_gpu():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Check results: OK" in r.stdout
     assert "single assignment" in r.stdout and "deadlock" in r.stdout
+
+
+FIN_EXE = os.path.join(os.path.dirname(H.LIB_PATH), "tests", "device_finish")
+
+
+def test_device_finish_program_is_built():
+    assert os.path.exists(FIN_EXE), "run python -m hclib_amd.build"
+
+
+@pytest.mark.gpu
+def test_device_nested_finish_on_gpu():
+    """Nested finish inside device tasks (include/hclib_hip/hx_finish.h):
+    fib as test/fib/fib.c writes it (FINISH + continuation) as a user kind
+    through run_tasks, fib(0..27) against fib_iter with exact task and
+    continuation counts; test/cpp/nested_finish.cpp's 100 iterations x 4
+    nested finishes, every finish ending after everything inside it."""
+    r = subprocess.run([FIN_EXE], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Check results: OK" in r.stdout
+    assert "fib(27) = 196418" in r.stdout and "nested finish: 100 iterations x 4" in r.stdout

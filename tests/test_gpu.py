@@ -178,6 +178,27 @@ def test_uts_t3l_shards_sum_to_tree(golden):
     assert max(p["max_depth"] for p in parts) == pub["depth"]
 
 
+@pytest.mark.parametrize("name,split", [("T3L", 64), ("T1XL", 7)])
+def test_uts_bench_partition_8_ranks(golden, name, split, capsys):
+    """bench.py's exact N=8 partition (split depth 64 for T3L, 7 for T1XL;
+    shard = node-state hash mod 8, bench.py:46-69), every shard through
+    hclib_hip_uts_search as its rank runs it: the shards sum to the
+    published tree (test/uts/sample_trees.sh:42-43, :50-51) and each
+    shard's kernel time is printed. T3L is span-bound: the shard holding
+    the deepest chain takes about the whole-tree time on its own."""
+    pub = golden("uts_goldens.json")["published"][name]
+    parts = [H.uts(pub["args"], s, 8, split) for s in range(8)]
+    assert sum(p["nodes"] for p in parts) == pub["nodes"]
+    assert sum(p["leaves"] for p in parts) == pub["leaves"]
+    assert max(p["max_depth"] for p in parts) == pub["depth"]
+    whole = H.uts(pub["args"])
+    with capsys.disabled():
+        print(f"\n{name} split {split}: whole {whole['kernel_ms']:.2f} ms; shards (nodes, ms): " +
+              ", ".join(f"({p['nodes']}, {p['kernel_ms']:.2f})" for p in parts))
+    # the slowest shard is at most the whole search plus the replicated top
+    assert max(p["kernel_ms"] for p in parts) < 2.0 * whole["kernel_ms"] + 5.0
+
+
 def test_uts_other_shapes_vs_oracle():
     for args in ["-t 1 -a 1 -d 8 -b 3 -r 5", "-t 3 -d 6 -b 5 -r 3", "-t 0 -b 200 -q 0.19 -m 5 -r 11",
                  "-t 1 -a 3 -d 7 -b 4 -r 19 -g 3"]:
