@@ -79,7 +79,7 @@ EXPORTS_HIP = [
     "hclib_hip_init", "hclib_hip_finalize", "hclib_hip_last_error", "hclib_hip_num_cus",
     "hclib_hip_version", "hclib_hip_forasync", "hclib_hip_forasync_triad_f32",
     "hclib_hip_num_workers", "hclib_hip_uts_search", "hclib_hip_uts_num_children_host",
-    "hclib_hip_fib", "hclib_hip_sw", "hclib_hip_last_sched_counters",
+    "hclib_hip_fib", "hclib_hip_sw", "hclib_hip_last_sched_counters", "hclib_hip_last_narrow_counters",
     "hclib_hip_sw_band_begin", "hclib_hip_sw_band_rows", "hclib_hip_sw_band_end",
 ]
 
@@ -275,4 +275,11 @@ def last_sched_counters():
     """Counters of the last megakernel launch (see include/hclib_hip.h)."""
     out = (C.c_uint64 * 16)()
     lib().hclib_hip_last_sched_counters(out)
+    return list(out)
+
+
+def last_narrow_counters():
+    """Narrow-frontier loop of the last launch: batches, cycles, entries."""
+    out = (C.c_uint64 * 4)()
+    lib().hclib_hip_last_narrow_counters(out)
     return list(out)

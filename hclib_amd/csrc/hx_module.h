@@ -26,6 +26,7 @@ struct Module {
     size_t pool_bytes = 0;
     SchedGlobals *globals = nullptr;
     unsigned long long last_counters[16] = {};  // counters of the last megakernel launch
+    unsigned long long last_narrow[4] = {};     // SchedGlobals::narrow of the last launch
     // per-wave records of megakernel launches (WaveStat, hx_sched.h)
     WaveStat *wave_stats = nullptr;
     uint32_t wave_stats_cap = 0;

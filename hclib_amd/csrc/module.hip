@@ -112,6 +112,7 @@ int finish_sched(SchedGlobals *host_copy, const char *who) {
     const uint32_t nw_cap = m.wave_stats_cap;
     HX_HIP(hipStreamSynchronize(m.stream));
     memcpy(m.last_counters, host_copy->counters, sizeof(m.last_counters));
+    memcpy(m.last_narrow, host_copy->narrow, sizeof(m.last_narrow));
     // every wave of the grid leaves exactly once: counters[kCtrWaves] records
     uint64_t nw = host_copy->counters[kCtrWaves];
     if (nw > nw_cap) nw = nw_cap;
@@ -184,6 +185,10 @@ int hclib_hip_num_cus(void) { return g_mod.inited ? g_mod.num_cus : 0; }
 
 void hclib_hip_last_sched_counters(uint64_t out[16]) {
     for (int i = 0; i < 16; ++i) out[i] = g_mod.last_counters[i];
+}
+
+void hclib_hip_last_narrow_counters(uint64_t out[4]) {
+    for (int i = 0; i < 4; ++i) out[i] = g_mod.last_narrow[i];
 }
 
 int hclib_hip_last_wave_stats(hclib_hip_wave_stats_t *out, int max) {

@@ -169,13 +169,12 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
         int n = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) n += c.thr16[k] <= r ? 1 : 0;
-        if (n == 16) {  // rare: thresholds 17..100 (table 0 in LDS)
+        if (n == 16) {  // rare: thresholds 17..100 of table 0 (device memory, L2-resident)
             int lo = 16, hi = 100;
-#pragma unroll
             for (int s = 0; s < 7; ++s) {
                 int mid = (lo + hi + 1) >> 1;
                 if (lo < hi) {
-                    if (s_thr[mid] <= r) lo = mid;
+                    if (c.thr[mid] <= r) lo = mid;
                     else hi = mid - 1;
                 }
             }
@@ -209,15 +208,19 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
     return lo;
 }
 
+// ring items per wave (CAP) and the pieces a task's children are pushed as:
+// BIN trees 1024 / 8 (m <= 8 children keep every batch uniform: the register
+// carry); GEO trees 512 / 5 by default (16 KiB: 8 waves per CU resident),
+// 256 / 1 (8 KiB) and 1024 / 8 as measured alternatives (HCLIB_HIP_UTS_RING)
+template <int CAP>
+constexpr int uts_pieces() { return CAP >= 1024 ? 8 : (CAP >= 512 ? 5 : 1); }
+
 // FEAT = 0: plain search; 1: sharded (nshards > 1) and/or per-level histogram
-template <int MODE, int FEAT>
+template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512)>
 struct UtsKind {
     // template = the node {state[5], height}; an item = its children [k, kend)
     static constexpr int kTmplWords = 6;
-    // BIN trees spawn m <= 8 children: 8 pieces keep every batch uniform (the
-    // register carry); GEO trees take 5 pieces so their ring fits 512 items
-    // (16 KiB) and twice the waves stay resident per CU
-    static constexpr int kPieces = MODE == kUtsBin ? 8 : 5;
+    static constexpr int kPieces = uts_pieces<CAP>();
     static constexpr int kWords = 8;
     static constexpr bool kPure = FEAT == 0;  // the histogram's atomics are side effects
     static constexpr bool kBoundedChildren = true;  // <= 100 (the root goes through roots())
@@ -280,19 +283,20 @@ struct UtsKind {
     }
 };
 
-// ring items per wave: 1024 (32 KiB of LDS) for BIN trees, 512 (16 KiB) for
-// the others (5 pieces per task: one batch pushes at most 64 * 7 items)
-template <int MODE>
-constexpr int uts_cap() { return MODE == kUtsBin ? 1024 : 512; }
-
-template <int MODE, int FEAT>
+template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512)>
 __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, SchedGlobals *g,
                                                    SchedConfig cfg) {
-    constexpr int kUtsCap = uts_cap<MODE>();
-    __shared__ WaveStack<UtsKind<MODE, FEAT>, kUtsCap> st;
+    constexpr int kUtsCap = CAP;
+    __shared__ WaveStack<UtsKind<MODE, FEAT, CAP>, kUtsCap> st;
     if (MODE == kUtsGeoFixed) {
-        for (int i = threadIdx.x; i < 128; i += 64) s_thr[i] = ctx.thr[i];
-        __syncthreads();
+        // the 16 thresholds compared per node live in VGPRs (wave-uniform
+        // values the compiler would otherwise keep in SGPRs, spilling the
+        // scheduler's scalar state around the batch loop)
+        UtsCtx lc = ctx;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) asm volatile("v_mov_b32 %0, %1" : "=v"(lc.thr16[k]) : "s"(ctx.thr16[k]));
+        run_worker<UtsKind<MODE, FEAT, CAP>, kUtsCap>(lc, pool, g, cfg, st, blockIdx.x == 0);
+        return;
     }
     if (MODE == kUtsRulesLds) {
         // the per-node rule lookup becomes LDS-latency (no dependent HBM/L2 loads)
@@ -300,7 +304,7 @@ __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, Sc
         for (int i = threadIdx.x; i < ctx.nthr; i += 64) s_thr[i] = ctx.thr[i];
         __syncthreads();
     }
-    run_worker<UtsKind<MODE, FEAT>, kUtsCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
+    run_worker<UtsKind<MODE, FEAT, CAP>, kUtsCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
 }
 
 // ------------------------------------------------------ host: rules/tables
@@ -577,19 +581,39 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // fewer hand-offs); throughput-bound GEO trees with 4
     const bool bin = params->type == 0 && T.rules.size() == 2 && T.rules[1].x == 1 && T.stationary;
     const bool geo_fixed = !bin && geo_depth > 0 && env_int("HCLIB_HIP_UTS_GEO_FIXED", 1);
+    // waves per CU: span-bound BIN trees run fastest with 2 (fewer idle
+    // pollers, fewer hand-offs); GEO trees are throughput-bound and fill 8
+    // (the 512-item rings leave room for them) once they are large — a
+    // small tree (T1, ~4 M nodes in 1 ms) loses more to spreading its few
+    // first levels over 2048 waves than it gains (profiles/r02/
+    // sweep_t1xl_waves_geo.log: T1XL 90 -> 52 ms from 4 to 8, T1 1.0 ->
+    // 1.45 ms). Size estimate: b_0^gen_mx nodes for the fixed shape.
+    int wpc_default = 2, ring_default = 512;
+    if (!bin) {
+        const double est = (params->type == 1 && params->shape_fn == 3) ? pow(params->b_0, (double)params->gen_mx) : 1e9;
+        wpc_default = est >= 3e7 ? 8 : 4;
+        // and a small tree runs faster on 256-item rings (one piece per task:
+        // the frontier fans out by range splitting) at 4 waves per CU: T1
+        // 0.98 -> 0.75 ms; a large one slower (T1XL 52 -> 70 ms),
+        // profiles/r02/sweep_t1_ring_waves.log, sweep_t1xl_ring_waves.log
+        ring_default = est >= 3e7 ? 512 : 256;
+    }
     const int grid = env_int("HCLIB_HIP_GRID", 0) > 0
                          ? env_int("HCLIB_HIP_GRID", 0)
-                         : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", bin ? 2 : 8);
+                         : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", wpc_default);
     SchedConfig cfg;
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_SPILL_HI", 512);
-    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", 96);
+    // BIN trees with the narrow-frontier loop give work away from 72 items
+    // (just over one batch: a wave keeps at most ~one batch of a narrow
+    // frontier, T3L 36.3 -> 35.0 ms, profiles/r02/t3l_knobs.log); GEO at 96
+    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", bin ? 72 : 96);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
     // hunger read every 32 batches, every 8 while many waves are hungry
     // (scripts/sweep_uts.py: T1 1.37 -> 1.07 ms, T1XL 101 -> 97 ms, T3L even)
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", 32);
-    cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 1);
+    cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     const bool feat = nshards > 1 || max_levels > 0;
@@ -602,7 +626,13 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         {k_uts_search<kUtsBin, 0>, k_uts_search<kUtsBin, 1>},
         {k_uts_search<kUtsGeoFixed, 0>, k_uts_search<kUtsGeoFixed, 1>},
     };
-    hipLaunchKernelGGL(kernels[mode][feat ? 1 : 0], dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
+    uts_kernel_t kern = kernels[mode][feat ? 1 : 0];
+    if (mode == kUtsGeoFixed && !feat) {  // ring-size variants of the fixed-shape GEO search
+        const int ring = env_int("HCLIB_HIP_UTS_RING", ring_default);
+        if (ring == 256) kern = k_uts_search<kUtsGeoFixed, 0, 256>;
+        else if (ring == 1024) kern = k_uts_search<kUtsGeoFixed, 0, 1024>;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
     HX_HIP(hipGetLastError());
     HX_HIP(hipEventRecord(m.ev1, m.stream));
     SchedGlobals gl;

@@ -87,6 +87,9 @@ typedef struct {
     uint64_t stolen_from[8]; /* chunks taken from each XCD's deques */
 } hclib_hip_wave_stats_t;
 int hclib_hip_last_wave_stats(hclib_hip_wave_stats_t *out, int max);
+/* The narrow-frontier carry loop of the last launch (hx_sched.h): [0]
+ * batches run in it, [1] shader-clock cycles spent in it, [2] entries. */
+void hclib_hip_last_narrow_counters(uint64_t out[4]);
 
 /* L2 atomic-throughput calibration: the saturated rate (million atomic
  * ops per second, whole GPU) of one access shape the runtime's atomics use,

@@ -84,6 +84,7 @@ struct alignas(256) SchedGlobals {
     unsigned long long maxes[4];      // kind-specific reductions (atomic max)
     WaveStat *wave_stats;             // per-wave records (indexed by blockIdx.x), or null
     uint32_t wave_stats_cap;          // records available
+    unsigned long long narrow[4];     // narrow-frontier loop: [0] batches, [1] s_memtime cycles, [2] entries
 };
 
 // Diagnostic build (-DHX_STAMPS=1): per-phase s_memtime stamps, enabled at run
@@ -127,9 +128,10 @@ struct SchedConfig {
     uint32_t stamps;     // diagnostic: accumulate per-phase s_memtime cycles
     uint32_t hunger;     // batches between reads of the hunger signal (0: never give work
                          // away unless the ring is full)
-    uint32_t carry = 1;  // keep a uniform batch's outputs in registers as the next batch
+    uint32_t carry = 2;  // keep a uniform batch's outputs in registers as the next batch
                          // (no ring push / pop) while they fit one batch and no hungry
-                         // wave could take them (see run_worker)
+                         // wave could take them (see run_worker); 2 also runs narrow
+                         // frontiers in a tight carry-to-carry loop, 1 does not
 };
 
 // Kind concept:
@@ -382,6 +384,26 @@ __device__ __forceinline__ uint32_t rcp16(uint32_t mu) {
                    : (mu <= 6 ? (mu == 5 ? 13108u : 10923u) : (mu == 7 ? 9363u : 8192u));
 }
 
+// Register carry: output o of a uniform batch (every spawning lane spawned
+// mu children) is child o % mu of the spawning lane of rank o / mu. One
+// ds_permute tells rank r its source lane, two ds_bpermute hops bring the
+// template to lane o.
+template <int TW>
+__device__ __forceinline__ void carry_permute(unsigned long long spawn, uint32_t mu, uint32_t nch,
+                                              const uint32_t *child, uint32_t *ctmpl, uint32_t &ck) {
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t nsp = (uint32_t)__builtin_popcountll(spawn);
+    const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(spawn >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
+    const uint32_t dst = nch != 0 ? rk : nsp + (lane - rk);
+    const int src_of_rank = __builtin_amdgcn_ds_permute((int)(dst * 4u), (int)lane);
+    const uint32_t r = (lane * rcp16(mu)) >> 16;  // lane / mu (lane < 64, mu <= 8)
+    const int src = __builtin_amdgcn_ds_bpermute((int)(r * 4u), src_of_rank);
+#pragma unroll
+    for (int i = 0; i < TW; ++i) ctmpl[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(src * 4, (int)child[i]);
+    ck = lane - r * mu;
+}
+
 // Uniform push: no lane has a residual range and every lane that spawned a
 // task spawned exactly `mu` (<= kPieces) children — every BIN-tree batch
 // after the root fan-out, every fib batch. Group starts are then
@@ -489,6 +511,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     if (lane < 8) st.stolen_from[lane] = 0;
     uint32_t n_exec = 0, n_spawn = 0;          // per lane: tasks run, children created
     unsigned long long items_stolen = 0;
+    unsigned long long n_narrow = 0, cyc_narrow = 0, n_narrow_in = 0;
     // register carry: the previous batch's `carry` outputs, lane o holding
     // item o (template ctmpl, child index ck); they form the front of the
     // next batch instead of round-tripping through the LDS ring
@@ -705,22 +728,73 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             const uint32_t hungry0 = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
             if (cfg.carry && uniform && tout > 0 && tout <= (uint32_t)kWaveSize &&
                 !(hungry0 > 0 && (top - bot) + tout >= cfg.spill_lo)) {
-                const uint32_t nsp = (uint32_t)__builtin_popcountll(spawn);
-                const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi(
-                    (uint32_t)(spawn >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
-                const uint32_t dst = nch != 0 ? rk : nsp + ((uint32_t)lane - rk);
-                const int src_of_rank = __builtin_amdgcn_ds_permute((int)(dst * 4u), lane);
-                const uint32_t rcp = rcp16(mu);
-                const uint32_t o = (uint32_t)lane;
-                const uint32_t r = (o * rcp) >> 16;  // o / mu (o < 64, mu <= 8)
-                const int src = __builtin_amdgcn_ds_bpermute((int)(r * 4u), src_of_rank);
-#pragma unroll
-                for (int i = 0; i < TW; ++i)
-                    ctmpl[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(src * 4, (int)child[i]);
-                ck = o - r * mu;
+                carry_permute<TW>(spawn, mu, nch, child, ctmpl, ck);
                 carry = tout;
                 if (HX_STAMPS && cfg.stamps) cyc_push += __builtin_amdgcn_s_memtime() - ts0;
                 if (HX_STAMPS && cfg.stamps) t_batch = __builtin_amdgcn_s_memtime();
+                // Narrow frontier (span-bound trees): the ring is empty and no
+                // hunger can stop a carry of at most one batch (spill_lo above
+                // it), so the chain runs in a tight loop of its own: process the
+                // carried items, carry their children, nothing else — no ring,
+                // no hunger reads, no spill checks. It leaves when the batch has
+                // no children (the wave goes idle at the loop top) or outputs
+                // that do not carry (non-uniform, or more than one batch): those
+                // go onto the empty ring and the main loop takes over.
+                if (cfg.carry > 1 && top == bot && cfg.spill_lo > (uint32_t)kWaveSize && !(HX_STAMPS && cfg.stamps)) {
+                    const unsigned long long tn0 = __builtin_amdgcn_s_memtime();
+                    const unsigned long long nb0 = nbatch;
+                    while (true) {
+                        const bool h = (uint32_t)lane < carry;
+                        uint32_t ch2[TW];
+                        int c2 = 0;
+                        if constexpr (Kind::kPure) {
+                            c2 = Kind::process(ctx, acc, ctmpl, ck, ch2, &g->err, h);
+                        } else {
+                            if (h) c2 = Kind::process(ctx, acc, ctmpl, ck, ch2, &g->err, true);
+                        }
+                        ++nbatch;
+                        uint32_t u2 = c2 > 0 ? (uint32_t)c2 : 0u;
+                        if (!Kind::kBoundedChildren && u2 >= kMaxChildren) {
+                            dev_error(&g->err, kErrBadTask);
+                            u2 = 0;
+                        }
+                        n_exec += h ? 1u : 0u;
+                        n_spawn += h ? u2 : 0u;
+                        const uint32_t n2 = u2 > (uint32_t)kPieces ? (uint32_t)kPieces : u2;
+                        const unsigned long long sp2 = __ballot(n2 != 0);
+                        if (!sp2) {
+                            carry = 0;
+                            break;
+                        }
+                        const uint32_t mu2 = (uint32_t)__builtin_amdgcn_readlane((int)n2, __builtin_ctzll(sp2));
+                        const bool uni2 = __ballot(u2 > (uint32_t)kPieces || (n2 != 0 && n2 != mu2)) == 0;
+                        const uint32_t rk2 = (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(sp2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sp2, 0u));
+                        if (uni2) {
+                            const uint32_t t2 = mu2 * (uint32_t)__builtin_popcountll(sp2);
+                            if (t2 <= (uint32_t)kWaveSize) {
+                                carry_permute<TW>(sp2, mu2, n2, ch2, ctmpl, ck);
+                                carry = t2;
+                                continue;
+                            }
+                            // more than one batch: onto the empty ring
+                            push_uniform<Kind, CAP>(st, top, mu2 * rk2, t2, mu2, n2 != 0, ch2);
+                            top += t2;
+                        } else {
+                            const int P2 = wave_scan_add((int)n2);
+                            const uint32_t t2 = (uint32_t)lane63(P2);
+                            push_outputs<Kind, CAP>(st, top, (uint32_t)(P2 - (int)n2), t2, 0u, u2, n2, ctmpl, ch2,
+                                                    ck, ck + 1, tag);
+                            tag += 16;
+                            top += t2;
+                        }
+                        carry = 0;
+                        break;
+                    }
+                    n_narrow += nbatch - nb0;
+                    cyc_narrow += __builtin_amdgcn_s_memtime() - tn0;
+                    ++n_narrow_in;
+                }
                 continue;
             }
         }
@@ -812,6 +886,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             }
             ((unsigned long long *)&g->wave_stats[gid])[lane] = v;
         }
+    }
+    if (lane == 0 && n_narrow_in) {
+        add_agent(&g->narrow[0], n_narrow);
+        add_agent(&g->narrow[1], cyc_narrow);
+        add_agent(&g->narrow[2], n_narrow_in);
     }
     if (lane == 0) {
         add_agent(&g->counters[kCtrBusyCycles], cyc_busy);

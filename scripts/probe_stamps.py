@@ -9,14 +9,14 @@ import torch  # noqa: E402,F401
 import hclib_amd as H  # noqa: E402
 
 H.init(0)
-for name, args in [("T3L", "-t 0 -b 2000 -q 0.200014 -m 5 -r 7"), ("T1L", "-t 1 -a 3 -d 13 -b 4 -r 29"),
+for name, args in [("T3L", "-t 0 -b 2000 -q 0.200014 -m 5 -r 7"), ("T1XL", "-t 1 -a 3 -d 15 -b 4 -r 29"),
                    ("T1", "-t 1 -a 3 -d 10 -b 4 -r 19")]:
     r = H.uts(args)
     c = H.last_sched_counters()
     nb = max(1, c[13])
-    print(f"{name}: ms={r['kernel_ms']:.2f} batches={nb} cycles/batch: form={c[7]/nb:.0f} "
-          f"process={c[8]/nb:.0f} busy={c[9]/nb:.0f} spill={c[11]/nb:.0f} idle_total={c[10]:.3e}",
-          flush=True)
+    print(f"{name}: ms={r['kernel_ms']:.2f} batches={nb} nodes/batch={r['nodes']/nb:.1f} cycles/batch: "
+          f"form={c[7]/nb:.0f} process={c[8]/nb:.0f} push={c[4]/nb:.0f} busy={c[9]/nb:.0f} "
+          f"spill={c[11]/nb:.0f} idle_total={c[10]:.3e} busy_frac={c[9]/max(1,c[9]+c[10]):.3f}", flush=True)
 v, st = H.fib(30)
 c = H.last_sched_counters()
 nb = max(1, c[13])
