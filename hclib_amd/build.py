@@ -35,7 +35,8 @@ CFLAGS = [
 ]
 
 
-VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "strict": ["-DHX_STRICT_HANDOFF=1"]}
+VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "strict": ["-DHX_STRICT_HANDOFF=1"],
+            "narrow_noinline": ["-DHX_NARROW_NOINLINE=1"]}
 
 
 def _hash(paths, cflags):

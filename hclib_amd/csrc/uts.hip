@@ -215,20 +215,25 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
 template <int CAP>
 constexpr int uts_pieces() { return CAP >= 1024 ? 8 : (CAP >= 512 ? 5 : 1); }
 
-// FEAT = 0: plain search; 1: sharded (nshards > 1) and/or per-level histogram
+// FEAT = 0: plain search; 1: sharded (nshards > 1) and/or per-level histogram;
+// 2: diagnostic trace (HCLIB_HIP_UTS_TRACE=1): per depth, the earliest
+// s_memrealtime (100 MHz) at which any wave reached it, recorded by a wave
+// only when its own deepest depth grows (the level_hist array receives
+// these times instead of counts)
 template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512)>
 struct UtsKind {
     // template = the node {state[5], height}; an item = its children [k, kend)
     static constexpr int kTmplWords = 6;
     static constexpr int kPieces = uts_pieces<CAP>();
     static constexpr int kWords = 8;
-    static constexpr bool kPure = FEAT == 0;  // the histogram's atomics are side effects
+    static constexpr bool kPure = FEAT != 1;  // the histogram's atomics are side effects (the trace stamps only from lane 0)
     static constexpr bool kBoundedChildren = true;  // <= 100 (the root goes through roots())
     using Ctx = UtsCtx;
     struct Acc {
         // per lane: at most one node per batch, so 32 bits last 4G batches
         uint32_t nodes = 0, leaves = 0;
         uint32_t maxd = 0;
+        uint32_t trace_seen = 0;  // FEAT 2: the deepest depth this wave has stamped
         __device__ void flush(SchedGlobals *g) {
             unsigned long long n = wave_sum((unsigned long long)nodes),
                                l = wave_sum((unsigned long long)leaves);
@@ -271,7 +276,16 @@ struct UtsKind {
         acc.nodes += counted ? 1u : 0u;
         acc.leaves += (counted && nc <= 0) ? 1u : 0u;
         acc.maxd = (counted && (uint32_t)h1 > acc.maxd) ? (uint32_t)h1 : acc.maxd;
-        if (FEAT && counted && c.hist && h1 < c.hist_levels) atomicAdd(&c.hist[h1], 1ull);
+        if (FEAT == 1 && counted && c.hist && h1 < c.hist_levels) atomicAdd(&c.hist[h1], 1ull);
+        if (FEAT == 2 && c.hist) {
+            const uint32_t dm = wave_max(counted ? (uint32_t)h1 : 0u);
+            if (dm > acc.trace_seen) {
+                acc.trace_seen = dm;
+                if (lane_id() == 0 && (int)dm < c.hist_levels)
+                    __hip_atomic_fetch_min(&c.hist[dm], (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                                           __ATOMIC_RELAXED, HX_AGENT);
+            }
+        }
         if (!valid) nc = 0;
         child[0] = ch[0];
         child[1] = ch[1];
@@ -519,7 +533,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
                                     int split_depth, hclib_hip_uts_result_t *result,
                                     uint64_t *level_hist, int max_levels) {
     if (!params || !result || nshards < 1 || shard < 0 || shard >= nshards || max_levels < 0 ||
-        max_levels > 1024 || (nshards > 1 && split_depth < 1)) {
+        max_levels > 65536 || (nshards > 1 && split_depth < 1)) {
         set_error("hclib_hip_uts_search: invalid arguments");
         return HCLIB_HIP_EINVAL;
     }
@@ -540,7 +554,8 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         (unsigned long long *)(dp + ((rb + 255) & ~(size_t)255) + ((tb + 255) & ~(size_t)255));
     HX_HIP(hipMemcpyAsync(d_rules, T.rules.data(), rb, hipMemcpyHostToDevice, m.stream));
     HX_HIP(hipMemcpyAsync(d_thr, T.thr.data(), tb, hipMemcpyHostToDevice, m.stream));
-    if (max_levels) HX_HIP(hipMemsetAsync(d_hist, 0, hb, m.stream));
+    const bool trace = env_int("HCLIB_HIP_UTS_TRACE", 0) != 0 && max_levels > 0;
+    if (max_levels) HX_HIP(hipMemsetAsync(d_hist, trace ? 0xff : 0, hb, m.stream));
 
     UtsCtx ctx;
     memcpy(ctx.root, T.root, sizeof(ctx.root));
@@ -614,6 +629,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // (scripts/sweep_uts.py: T1 1.37 -> 1.07 ms, T1XL 101 -> 97 ms, T3L even)
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", 32);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
+    cfg.backoff = (uint32_t)env_int("HCLIB_HIP_BACKOFF", 16);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     const bool feat = nshards > 1 || max_levels > 0;
@@ -627,6 +643,14 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         {k_uts_search<kUtsGeoFixed, 0>, k_uts_search<kUtsGeoFixed, 1>},
     };
     uts_kernel_t kern = kernels[mode][feat ? 1 : 0];
+    if (trace) {
+        if (mode != kUtsBin || nshards > 1) {
+            (void)hipFree(dmem);
+            set_error("hclib_hip_uts_search: the depth trace is for unsharded BIN trees");
+            return HCLIB_HIP_EINVAL;
+        }
+        kern = k_uts_search<kUtsBin, 2>;
+    }
     if (mode == kUtsGeoFixed && !feat) {  // ring-size variants of the fixed-shape GEO search
         const int ring = env_int("HCLIB_HIP_UTS_RING", ring_default);
         if (ring == 256) kern = k_uts_search<kUtsGeoFixed, 0, 256>;

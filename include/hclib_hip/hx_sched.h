@@ -128,6 +128,7 @@ struct SchedConfig {
     uint32_t stamps;     // diagnostic: accumulate per-phase s_memtime cycles
     uint32_t hunger;     // batches between reads of the hunger signal (0: never give work
                          // away unless the ring is full)
+    uint32_t backoff = 16;  // longest idle s_sleep (1, 4 or 16 units of 64 clocks)
     uint32_t carry = 2;  // keep a uniform batch's outputs in registers as the next batch
                          // (no ring push / pop) while they fit one batch and no hungry
                          // wave could take them (see run_worker); 2 also runs narrow
@@ -481,6 +482,95 @@ __device__ __forceinline__ void push_outputs(WaveStack<Kind, CAP> &st, uint32_t 
     }
 }
 
+// Narrow frontier (span-bound trees): the ring is empty and no hunger can
+// stop a carry of at most one batch (spill_lo above it), so the chain runs in
+// a loop of its own: process the carried items, carry their children,
+// nothing else — no ring, no hunger reads, no spill checks. It returns when a
+// batch has no children (the wave goes idle) or outputs that do not carry
+// (non-uniform, or more than one batch): those go onto the empty ring and
+// the main loop takes over. A separate (not inlined) function so the
+// compiler keeps its own copy of the task body instead of sharing the main
+// loop's, whose scheduler state would otherwise ride along every iteration.
+template <int TW>
+struct NarrowState {
+    uint32_t ctmpl[TW];
+    uint32_t ck, carry, top, tag, n_exec, n_spawn, batches;
+};
+
+#ifndef HX_NARROW_NOINLINE
+#define HX_NARROW_NOINLINE 0  // measured: inlined 34.1-34.5 ms vs 35.7-36.3 ms on T3L (profiles/r02/narrow_inline_ab.log)
+#endif
+#if HX_NARROW_NOINLINE
+#define HX_NARROW_ATTR __attribute__((noinline))
+#else
+#define HX_NARROW_ATTR __forceinline__
+#endif
+template <class Kind, int CAP>
+__device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
+    const typename Kind::Ctx &ctx_ref, typename Kind::Acc &acc_ref, uint32_t *err, WaveStack<Kind, CAP> &st,
+    NarrowState<Kind::kTmplWords> ns) {
+    constexpr int TW = Kind::kTmplWords;
+    constexpr int kPieces = pieces_of<Kind>();
+    // private copies: through the references every iteration would reload
+    // the parameters and store the counters (flat memory, waited on mid-task)
+    const typename Kind::Ctx ctx = ctx_ref;
+    typename Kind::Acc acc = acc_ref;
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t carry = lane0(ns.carry), batches = 0;
+    while (true) {
+        const bool h = lane < carry;
+        uint32_t ch2[TW];
+        int c2 = 0;
+        if constexpr (Kind::kPure) {
+            c2 = Kind::process(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h);
+        } else {
+            if (h) c2 = Kind::process(ctx, acc, ns.ctmpl, ns.ck, ch2, err, true);
+        }
+        ++batches;
+        uint32_t u2 = c2 > 0 ? (uint32_t)c2 : 0u;
+        if (!Kind::kBoundedChildren && u2 >= kMaxChildren) {
+            dev_error(err, kErrBadTask);
+            u2 = 0;
+        }
+        ns.n_exec += h ? 1u : 0u;
+        ns.n_spawn += h ? u2 : 0u;
+        const uint32_t n2 = u2 > (uint32_t)kPieces ? (uint32_t)kPieces : u2;
+        const unsigned long long sp2 = __ballot(n2 != 0);
+        if (!sp2) {
+            carry = 0;
+            break;
+        }
+        const uint32_t mu2 = (uint32_t)__builtin_amdgcn_readlane((int)n2, __builtin_ctzll(sp2));
+        const bool uni2 = __ballot(u2 > (uint32_t)kPieces || (n2 != 0 && n2 != mu2)) == 0;
+        if (uni2) {
+            const uint32_t t2 = mu2 * (uint32_t)__builtin_popcountll(sp2);
+            if (t2 <= (uint32_t)kWaveSize) {
+                carry_permute<TW>(sp2, mu2, n2, ch2, ns.ctmpl, ns.ck);
+                carry = t2;
+                continue;
+            }
+            // more than one batch: onto the empty ring
+            const uint32_t rk2 = (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(sp2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sp2, 0u));
+            push_uniform<Kind, CAP>(st, ns.top, mu2 * rk2, t2, mu2, n2 != 0, ch2);
+            ns.top += t2;
+        } else {
+            const int P2 = wave_scan_add((int)n2);
+            const uint32_t t2 = (uint32_t)lane63(P2);
+            push_outputs<Kind, CAP>(st, ns.top, (uint32_t)(P2 - (int)n2), t2, 0u, u2, n2, ns.ctmpl, ch2, ns.ck,
+                                    ns.ck + 1, ns.tag);
+            ns.tag += 16;
+            ns.top += t2;
+        }
+        carry = 0;
+        break;
+    }
+    ns.carry = carry;
+    ns.batches = batches;
+    acc_ref = acc;
+    return ns;
+}
+
 template <class Kind, int CAP>
 __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, SchedGlobals *g,
                            const SchedConfig &cfg, WaveStack<Kind, CAP> &st, bool seed_roots) {
@@ -620,8 +710,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 break;
             }
             // back off so idle pollers do not saturate the deque heads
-            if (spins < 8) __builtin_amdgcn_s_sleep(1);
-            else if (spins < 64) __builtin_amdgcn_s_sleep(4);
+            // (cfg.backoff: the longest sleep, 16 = 1024 clocks)
+            if (spins < 8 || cfg.backoff <= 1) __builtin_amdgcn_s_sleep(1);
+            else if (spins < 64 || cfg.backoff <= 4) __builtin_amdgcn_s_sleep(4);
             else __builtin_amdgcn_s_sleep(16);
             continue;
         }
@@ -742,56 +833,27 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 // go onto the empty ring and the main loop takes over.
                 if (cfg.carry > 1 && top == bot && cfg.spill_lo > (uint32_t)kWaveSize && !(HX_STAMPS && cfg.stamps)) {
                     const unsigned long long tn0 = __builtin_amdgcn_s_memtime();
-                    const unsigned long long nb0 = nbatch;
-                    while (true) {
-                        const bool h = (uint32_t)lane < carry;
-                        uint32_t ch2[TW];
-                        int c2 = 0;
-                        if constexpr (Kind::kPure) {
-                            c2 = Kind::process(ctx, acc, ctmpl, ck, ch2, &g->err, h);
-                        } else {
-                            if (h) c2 = Kind::process(ctx, acc, ctmpl, ck, ch2, &g->err, true);
-                        }
-                        ++nbatch;
-                        uint32_t u2 = c2 > 0 ? (uint32_t)c2 : 0u;
-                        if (!Kind::kBoundedChildren && u2 >= kMaxChildren) {
-                            dev_error(&g->err, kErrBadTask);
-                            u2 = 0;
-                        }
-                        n_exec += h ? 1u : 0u;
-                        n_spawn += h ? u2 : 0u;
-                        const uint32_t n2 = u2 > (uint32_t)kPieces ? (uint32_t)kPieces : u2;
-                        const unsigned long long sp2 = __ballot(n2 != 0);
-                        if (!sp2) {
-                            carry = 0;
-                            break;
-                        }
-                        const uint32_t mu2 = (uint32_t)__builtin_amdgcn_readlane((int)n2, __builtin_ctzll(sp2));
-                        const bool uni2 = __ballot(u2 > (uint32_t)kPieces || (n2 != 0 && n2 != mu2)) == 0;
-                        const uint32_t rk2 = (uint32_t)__builtin_amdgcn_mbcnt_hi(
-                            (uint32_t)(sp2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sp2, 0u));
-                        if (uni2) {
-                            const uint32_t t2 = mu2 * (uint32_t)__builtin_popcountll(sp2);
-                            if (t2 <= (uint32_t)kWaveSize) {
-                                carry_permute<TW>(sp2, mu2, n2, ch2, ctmpl, ck);
-                                carry = t2;
-                                continue;
-                            }
-                            // more than one batch: onto the empty ring
-                            push_uniform<Kind, CAP>(st, top, mu2 * rk2, t2, mu2, n2 != 0, ch2);
-                            top += t2;
-                        } else {
-                            const int P2 = wave_scan_add((int)n2);
-                            const uint32_t t2 = (uint32_t)lane63(P2);
-                            push_outputs<Kind, CAP>(st, top, (uint32_t)(P2 - (int)n2), t2, 0u, u2, n2, ctmpl, ch2,
-                                                    ck, ck + 1, tag);
-                            tag += 16;
-                            top += t2;
-                        }
-                        carry = 0;
-                        break;
-                    }
-                    n_narrow += nbatch - nb0;
+                    NarrowState<TW> ns;
+#pragma unroll
+                    for (int i = 0; i < TW; ++i) ns.ctmpl[i] = ctmpl[i];
+                    ns.ck = ck;
+                    ns.carry = carry;
+                    ns.top = top;
+                    ns.tag = tag;
+                    ns.n_exec = n_exec;
+                    ns.n_spawn = n_spawn;
+                    ns.batches = 0;
+                    ns = narrow_loop<Kind, CAP>(ctx, acc, &g->err, st, ns);
+#pragma unroll
+                    for (int i = 0; i < TW; ++i) ctmpl[i] = ns.ctmpl[i];
+                    ck = ns.ck;
+                    carry = lane0(ns.carry);
+                    top = lane0(ns.top);
+                    tag = lane0(ns.tag);
+                    n_exec = ns.n_exec;
+                    n_spawn = ns.n_spawn;
+                    nbatch += lane0(ns.batches);
+                    n_narrow += lane0(ns.batches);
                     cyc_narrow += __builtin_amdgcn_s_memtime() - tn0;
                     ++n_narrow_in;
                 }
