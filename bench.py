@@ -116,11 +116,22 @@ def measure_triad(H, reps=20, n=1 << 28, sync=None):
     e1.record(st)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
+    # per-launch spread (one event pair per launch, same stream): the box's
+    # HBM rate varies run to run, min / median say how much
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for s0, s1 in evs:
+        s0.record(st)
+        H.triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), 3.0, n, st.cuda_stream)
+        s1.record(st)
+    torch.cuda.synchronize()
+    per = sorted(s0.elapsed_time(s1) for s0, s1 in evs)
     ok = bool(torch.equal(a, torch.add(b, torch.mul(c, 3.0))))
     del a, b, c, buf
     torch.cuda.empty_cache()
     algo = 12 * n  # read b, c; write a (write-allocate not counted)
-    return {"ms": ms, "gbs": algo / ms / 1e6, "bytes": algo, "bit_exact": ok}
+    return {"ms": ms, "gbs": algo / ms / 1e6, "bytes": algo, "bit_exact": ok,
+            "launch_ms_min": per[0], "launch_ms_median": per[len(per) // 2],
+            "gbs_best": algo / per[0] / 1e6, "gbs_median": algo / per[len(per) // 2] / 1e6}
 
 
 def measure_atomics(H, fib_stats):
@@ -393,6 +404,10 @@ def main():
             "traffic": traffic,
             "algorithmic_bytes_per_launch": tri["bytes"],
             "avg_launch_ms": tri["ms"],
+            "launch_ms_min": tri["launch_ms_min"],
+            "launch_ms_median": tri["launch_ms_median"],
+            "frac_best_launch": tri["gbs_best"] / HBM_PEAK_GBS,
+            "frac_median_launch": tri["gbs_median"] / HBM_PEAK_GBS,
             "bit_exact": tri["bit_exact"],
         }
         # UTS kernel bound: span (critical path of dependent SHA-1s)

@@ -91,6 +91,69 @@ __global__ __launch_bounds__(THREADS) void k_triad_f32(float *__restrict__ a,
     }
 }
 
+// LDS-DMA form (MI355X_MICROARCH.md "ldsdma-fill": global_load_lds streams
+// reach a higher chip rate than loads to VGPRs): every wave streams its own
+// chunks of 64 float4 (1 KiB per array), DEPTH chunks of b and c in flight
+// in a per-wave LDS ring; a chunk is computed from LDS once its two DMAs
+// have landed (counted vmcnt) and a is stored non-temporally. AUX: the DMA's
+// cache-policy bits (2 = nt).
+template <int DEPTH, int AUX>
+__global__ __launch_bounds__(256) void k_triad_lds(float *__restrict__ a, const float *__restrict__ b,
+                                                   const float *__restrict__ c, float s, int64_t n4) {
+    __shared__ v4f ring[4][DEPTH][2][64];  // [wave][slot][b|c][lane]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + wave, nw = (int64_t)gridDim.x * 4;
+    const int64_t nchunks = n4 >> 6;  // whole 64-float4 chunks; the rest below
+    const v4f *b4 = reinterpret_cast<const v4f *>(b);
+    const v4f *c4 = reinterpret_cast<const v4f *>(c);
+    v4f *a4 = reinterpret_cast<v4f *>(a);
+    auto issue = [&](int64_t k, int slot) {
+        const int64_t i = (k * nw + gw) * 64 + lane;
+        __builtin_amdgcn_global_load_lds((const void *)&b4[i],
+                                         (__attribute__((address_space(3))) void *)&ring[wave][slot][0][0], 16, 0, AUX);
+        __builtin_amdgcn_global_load_lds((const void *)&c4[i],
+                                         (__attribute__((address_space(3))) void *)&ring[wave][slot][1][0], 16, 0, AUX);
+    };
+    // chunks of this wave: k = 0, 1, ... with (k * nw + gw) < nchunks
+    const int64_t mine = gw < nchunks ? (nchunks - gw + nw - 1) / nw : 0;
+    int64_t k = 0;
+    for (; k < DEPTH && k < mine; ++k) issue(k, (int)k);
+    for (int64_t j = 0; j < mine; ++j) {
+        const int slot = (int)(j % DEPTH);
+        // chunk j's two DMAs are the oldest outstanding ops: younger are the
+        // DMAs of up to DEPTH-1 later chunks and the stores of up to DEPTH-1
+        // earlier ones (stores count in vmcnt on gfx9)
+        // (in the first DEPTH iterations fewer stores are younger: at least
+        // 2 (DEPTH - 1) ops are; near the end fewer refills: wait for all)
+        if (mine - j < DEPTH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (j < DEPTH) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DEPTH - 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
+        const v4f vb = ring[wave][slot][0][lane], vc = ring[wave][slot][1][lane];
+        v4f r;
+        r.x = triad1(vb.x, vc.x, s);
+        r.y = triad1(vb.y, vc.y, s);
+        r.z = triad1(vb.z, vc.z, s);
+        r.w = triad1(vb.w, vc.w, s);
+        __builtin_nontemporal_store(r, &a4[(j * nw + gw) * 64 + lane]);
+        // the slot is refilled only after this wave's reads of it returned
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (k < mine) {
+            issue(k, slot);
+            ++k;
+        }
+    }
+    // the float4s past the last whole chunk
+    for (int64_t i = nchunks * 64 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const v4f vb = b4[i], vc = c4[i];
+        v4f r;
+        r.x = triad1(vb.x, vc.x, s);
+        r.y = triad1(vb.y, vc.y, s);
+        r.z = triad1(vb.z, vc.z, s);
+        r.w = triad1(vb.w, vc.w, s);
+        a4[i] = r;
+    }
+}
+
 typedef void (*triad_kernel_t)(float *, const float *, const float *, float, int64_t);
 
 template <int THREADS, bool CONTIG>
@@ -115,6 +178,16 @@ static triad_kernel_t triad_pick(int v) {
 // 8 = contiguous slice per workgroup, 16/32 = 512/1024 threads (else 256),
 // 64 / 128 = unroll 2 / 1 (nt stores; nt loads when bits 0-1 are 3)
 static triad_kernel_t triad_variant(int v, int *threads) {
+    if (v & 256) {  // LDS-DMA: bits 0-1 = depth 2/4/8/16, bit 2 = nt DMA
+        *threads = 256;
+        const bool nt = (v & 4) != 0;
+        switch (v & 3) {
+        case 0: return nt ? k_triad_lds<2, 2> : k_triad_lds<2, 0>;
+        case 1: return nt ? k_triad_lds<4, 2> : k_triad_lds<4, 0>;
+        case 2: return nt ? k_triad_lds<8, 2> : k_triad_lds<8, 0>;
+        default: return nt ? k_triad_lds<16, 2> : k_triad_lds<16, 0>;
+        }
+    }
     const bool contig = (v & 8) != 0;
     const int t = (v >> 4) & 3;
     *threads = t == 1 ? 512 : (t == 2 ? 1024 : 256);
@@ -225,12 +298,15 @@ extern "C" int hclib_hip_forasync_triad_f32(float *a, const float *b, const floa
     }
     const int64_t n4 = n / 4;
     if (n4 > 0) {
-        // measured best on MI355X (scripts/ubench/ub_triad.hip, scripts/probe_triad.py):
-        // one 256-thread workgroup per CU, non-temporal loads + stores, 2 (b, c)
-        // pairs per lane in flight = 16 KiB of loads per CU (32 KiB: -4 %)
-        const int bpc = env_int("HCLIB_HIP_TRIAD_BLOCKS_PER_CU", 1);
+        // measured best on MI355X (scripts/probe_triad2.py, profiles/r02/triad_variants.log):
+        // two 256-thread workgroups per CU, one (b, c) pair of non-temporal
+        // 16-B loads per lane in flight (16 KiB of loads per CU) and
+        // non-temporal stores: 6.22-6.26 TB/s, against 6.15-6.22 for one
+        // workgroup with two pairs; the LDS-DMA form (variants 256-263) and
+        // deeper pipelines measured no faster
+        const int bpc = env_int("HCLIB_HIP_TRIAD_BLOCKS_PER_CU", 2);
         int threads = kTriadThreads;
-        triad_kernel_t k = triad_variant(env_int("HCLIB_HIP_TRIAD_VARIANT", 67), &threads);
+        triad_kernel_t k = triad_variant(env_int("HCLIB_HIP_TRIAD_VARIANT", 131), &threads);
         int64_t grid = (int64_t)mod().num_cus * bpc;
         const int64_t need = (n4 + threads - 1) / threads;
         if (grid > need) grid = need;
