@@ -538,6 +538,206 @@ __global__ __launch_bounds__(64) void k_sw_rows(SwCtx c) {
     }
 }
 
+// ----------------------------------------------- multi-wave tile rows
+// Tile row as a workgroup of NW = th / 64 waves: wave w owns the 64 matrix
+// rows 64w .. 64w + 63 of the tile row (one row per lane) and sweeps the
+// band's columns left to right in ONE continuous anti-diagonal pipeline —
+// tile boundaries inside the row are only where granules are published, so
+// no wave pays a ramp per tile. Lane L computes column s - L at step s; the
+// cell above comes from lane L-1 by one DPP wave shift, lane 0's from the
+// wave above through an LDS ring (ring w + 1 = wave w's bottom row, written
+// by its lane 63 every step). Wave 0's ring is filled from the up tile row's
+// granules (or the boundary row); wave NW-1 publishes its ring as the tile
+// row's granules. Flow control: prod[w] = columns of ring w written,
+// cons[w] = columns of ring w read, both per 64-column chunk. NW waves run
+// on the CU's 4 SIMDs at once instead of one wave per tile row.
+constexpr int kSwRing = 512;  // columns per inter-wave ring (+1 wrap slot)
+constexpr int kSwRingStride = kSwRing + 4;
+
+__host__ __device__ inline size_t sw_band_lds_bytes(int nw) {
+    return (size_t)(nw + 1) * kSwRingStride * 4  // rings
+           + (size_t)nw * 128 * 4                 // per-wave dummy slots (lanes 0..62's ring writes)
+           + (size_t)nw * 1024                    // per-wave code rings: 4 byte-shifted copies, double-mapped
+           + 2 * 64 * 4;                          // prod / cons words
+}
+
+// the multi-wave kernel's shape: 64-row bands, 1..16 waves per tile row
+inline bool sw_band_ok(int th) { return th % 64 == 0 && th / 64 >= 1 && th / 64 <= 16; }
+
+__device__ __forceinline__ int lds_ld_acq(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st_rel(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// 64 steps of one wave's band from step s0. top4 = ring slots of columns
+// s0 .. s0 + 63 (lane-uniform, 16-byte aligned), code4 = this lane's
+// aligned code words for columns s0 - lane .. s0 - lane + 63 (4 codes each),
+// wb = this lane's write base (lane 63: the out ring's slot of column
+// s0 - 63; other lanes: their dummy slots). G-space cells (see sw_tile).
+// Operands of 4 steps are read two groups ahead, in program order before the
+// previous group's ring writes (LDS completes a wave's operations in order).
+template <bool MASK>
+__device__ __forceinline__ void sw_band_chunk(int s0, int ncols, const int *top4, const uint32_t *code4, int *wb,
+                                              uint32_t mrow, int &left, int &diag, int &out) {
+    const int lane = lane_id();
+    int4 tn = *(const int4 *)top4, tn2 = *(const int4 *)(top4 + 4);
+    uint32_t cn = code4[0], cn2 = code4[1];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const int4 tc = tn;
+        const uint32_t cc = cn;
+        tn = tn2;
+        cn = cn2;
+        if (m < 14) {
+            tn2 = *(const int4 *)(top4 + 4 * (m + 2));
+            cn2 = code4[m + 2];
+        }
+        // score bytes of the 4 columns (s2 row fixed per lane)
+        const uint32_t sc = __builtin_amdgcn_perm(0u, mrow, cc);
+        const int tv[4] = {tc.x, tc.y, tc.z, tc.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = 4 * m + j;
+            const int up = __builtin_amdgcn_update_dpp(tv[j], out, 0x138, 0xf, 0xf, false);
+            const int d = diag + (int)(int8_t)(sc >> (8 * j));
+            const int a = left > up ? left : up;
+            int h = a > d ? a : d;
+            if (MASK) {
+                const bool v = (unsigned)(s0 + k - lane) < (unsigned)ncols;
+                h = v ? h : left;
+                diag = v ? up : diag;
+            } else {
+                diag = up;
+            }
+            left = h;
+            out = h;
+            wb[k] = h;
+        }
+    }
+}
+
+__device__ bool sw_band_spin(const SwCtx &c, const int *flag, int want, unsigned long long t0) {
+    while (lds_ld_acq(flag) < want) {
+        if (ld_agent(c.err)) return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
+            if (lane_id() == 0) dev_error(c.err, kErrSpinTimeout);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+
+// One wave's band of tile row i over the band's columns (matrix columns
+// C0 + 1 .. C0 + ncols, C0 = j0 * tw). Returns false on a device error.
+__device__ bool sw_band_row(const SwCtx &c, int i, int w, int nw, int *rings, int *dummy, uint8_t *code_rings,
+                            int *prod, int *cons) {
+    const int lane = lane_id();
+    const int th = c.th, C0 = c.j0 * c.tw, ncols = (c.j1 - c.j0) * c.tw;
+    const size_t gstride = (size_t)c.ntw * c.tw;  // granules per tile row
+    int *ring_in = rings + (size_t)w * kSwRingStride, *ring_out = ring_in + kSwRingStride;
+    uint8_t *cr = code_rings + w * 1024;
+    const int r = i * th + w * 64 + lane + 1;  // this lane's matrix row
+    const uint32_t mrow = sw_row2(c.s2[r - 1]);
+    // G at (r, C0) and (r - 1, C0): the band's left column
+    auto left_h = [&](int row) {
+        return row == 0 ? -C0 : (c.j0 == 0 ? -row : ld_agent(&c.left_in[row - 1]));
+    };
+    int left = left_h(r) + r + C0;
+    int diag = left_h(r - 1) + (r - 1) + C0;
+    int out = 0;
+    int *wbase = lane == 63 ? ring_out : dummy + w * 128 + lane;
+    const int8_t *s1 = c.s1 + C0;
+    int code_nx = lane < ncols ? s1[lane] - 1 : 0;  // code of column s0 + lane
+    unsigned long long pf = 0;                      // wave 0: granule of column s0 + lane
+    const unsigned long long *gup = c.gbot + (size_t)(i - 1) * gstride + C0;
+    if (w == 0 && i > 0 && lane < ncols) pf = ld_agent(&gup[lane]);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int s0 = 0; s0 < ncols + 63; s0 += 64) {
+        const int slot = s0 & (kSwRing - 1);
+        // (a) this chunk's top row: columns s0 .. s0 + 63 in ring_in
+        if (w == 0) {
+            const int cc = s0 + lane;
+            const bool need = i > 0 && cc < ncols;
+            while (!__all(!need || (pf >> 32) == 1ull)) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
+                    if (lane == 0) dev_error(c.err, kErrSpinTimeout);
+                    return false;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                if (need) pf = ld_agent(&gup[cc]);
+            }
+            // tile row 0: G of the boundary row is 0 (H = -col)
+            ring_in[slot + lane] = need ? (int)(uint32_t)pf + i * th + (C0 + cc + 1) : 0;
+            if (i > 0 && cc + 64 < ncols) pf = ld_agent(&gup[cc + 64]);
+        } else {
+            const int want = s0 + 64 < ncols ? s0 + 64 : ncols;
+            if (!sw_band_spin(c, &prod[w], want, t0)) return false;
+        }
+        // (b) ring_out's slots for columns s0 - 63 .. s0 are free
+        if (w + 1 < nw && s0 + 1 - kSwRing > 0)
+            if (!sw_band_spin(c, &cons[w + 1], s0 + 1 - kSwRing, t0)) return false;
+        // (c) codes of columns s0 .. s0 + 63: copy o holds column x at byte
+        // (x + o) mod 128 (and + 128), so lane L reads aligned words from
+        // copy L mod 4
+        {
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                const int q = (s0 + lane + o) & 127;
+                cr[o * 256 + q] = (uint8_t)code_nx;
+                cr[o * 256 + q + 128] = (uint8_t)code_nx;
+            }
+            const int cn = s0 + 64 + lane;
+            code_nx = cn < ncols ? s1[cn] - 1 : 0;
+        }
+        const uint32_t *cb = (const uint32_t *)(cr + (lane & 3) * 256 + ((s0 - lane + (lane & 3)) & 127));
+        int *wb = wbase + (lane == 63 ? ((s0 - 63) & (kSwRing - 1)) : 0);
+        if (s0 >= 64 && s0 + 64 <= ncols)
+            sw_band_chunk<false>(s0, ncols, ring_in + slot, cb, wb, mrow, left, diag, out);
+        else
+            sw_band_chunk<true>(s0, ncols, ring_in + slot, cb, wb, mrow, left, diag, out);
+        // (e) lane 63's last column (s0) also at its own slot (the wrap slot fix)
+        if (lane == 63) ring_out[slot] = left;
+        // (f) publish: columns < s0 + 1 of ring_out, columns < s0 + 64 of ring_in read
+        if (lane == 0) {
+            lds_st_rel(&prod[w + 1], s0 + 1 < ncols ? s0 + 1 : ncols);
+            lds_st_rel(&cons[w], s0 + 64);
+        }
+        // (h) the last wave hands its bottom row to the next tile row
+        if (w == nw - 1) {
+            const int cc = s0 - 63 + lane;
+            if (cc >= 0 && cc < ncols) {
+                const int h = ring_out[cc & (kSwRing - 1)] - (i + 1) * th - (C0 + cc + 1);
+                st_agent(&c.gbot[(size_t)i * gstride + C0 + cc], (1ull << 32) | (unsigned long long)(uint32_t)h);
+            }
+        }
+    }
+    if (c.right_out) c.right_out[r - 1] = left - r - (C0 + ncols);
+    return true;
+}
+
+__global__ __launch_bounds__(1024) void k_sw_band_rows(SwCtx c) {
+    extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+    const int nw = (int)(blockDim.x >> 6), w = (int)(threadIdx.x >> 6);
+    int *rings = sw_lds;
+    int *dummy = rings + (size_t)(nw + 1) * kSwRingStride;
+    uint8_t *code_rings = (uint8_t *)(dummy + nw * 128);
+    int *prod = (int *)(code_rings + nw * 1024), *cons = prod + 64;
+    bool ok = true;
+    unsigned long long ntile = 0;
+    for (int i = c.i0 + (int)blockIdx.x; i < c.i1; i += gridDim.x) {
+        if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod[0..63], cons[0..63]
+        __syncthreads();
+        ok = sw_band_row(c, i, w, nw, rings, dummy, code_rings, prod, cons);
+        vm_drain();
+        if (__syncthreads_or(!ok)) break;  // every wave leaves together
+        ntile += (unsigned long long)(c.j1 - c.j0);
+    }
+    if (threadIdx.x == 0) add_agent(&c.stats[0], ntile);
+}
+
 // The generic device promise DAG (include/hclib_hip/hx_dag.h) driving the
 // reference's tile program as written: every tile is an async_await on three
 // futures (left tile's right column, up tile's bottom row, diagonal tile's
@@ -604,6 +804,9 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
                             2 * (size_t)(((th + 3) & ~3) * 4);
     const bool dag = sched && !strcmp(sched, "dag");
     const bool rows = !(sched && (!strcmp(sched, "queue") || dag)) && rows_lds <= 64 * 1024;
+    // multi-wave tile rows (th / 64 waves per workgroup) unless "rows1" asks
+    // for the one-wave-per-tile-row kernel
+    const bool band = rows && sw_band_ok(th) && !(sched && !strcmp(sched, "rows1"));
     const size_t nt = ntw * nth;
     const size_t b_s1 = ntw * tw, b_s2 = nth * th;
     const size_t b_bot = rows ? 0 : nt * tw * 4, b_right = rows ? 0 : nt * th * 4, b_c = nt * 4,
@@ -658,8 +861,9 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     } else {
         hipLaunchKernelGGL(k_sw_init, dim3(1024), dim3(256), 0, m.stream, c.deps, c.ready, c.ntw, c.nth);
     }
-    const size_t lds = 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + 68 * 4 + 2 * (size_t)((tw + 3) & ~3) + 16 +
-                       (rows ? 2 * (size_t)(((th + 3) & ~3) * 4) : 0);
+    const size_t lds = band ? sw_band_lds_bytes(th / 64)
+                            : 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + 68 * 4 + 2 * (size_t)((tw + 3) & ~3) + 16 +
+                                  (rows ? 2 * (size_t)(((th + 3) & ~3) * 4) : 0);
     if (lds > 160 * 1024) return fail((set_error("hclib_hip_sw: tile too large for LDS"), HCLIB_HIP_EINVAL));
     int per_cu = (int)((160 * 1024) / lds);
     // rows: one wave per CU owns tile rows (all resident, so every wait ends)
@@ -694,7 +898,12 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         if ((rc = hclib_hip_dag_end("hclib_hip_sw (dag)", nullptr, nullptr, &dst))) return fail(rc);
     } else {
         if ((rc = hip_check(hipEventRecord(m.ev0, m.stream), "event"))) return fail(rc);
-        if (rows && c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), lds, m.stream, c);
+        if (band) {
+            int g = (int)nth < m.num_cus ? (int)nth : m.num_cus;
+            if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_band_rows,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(k_sw_band_rows, dim3(g), dim3(th), lds, m.stream, c);
+        } else if (rows && c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), lds, m.stream, c);
         else if (rows) hipLaunchKernelGGL(k_sw_rows<false>, dim3(grid), dim3(64), lds, m.stream, c);
         else hipLaunchKernelGGL(k_sw, dim3(grid), dim3(64), lds, m.stream, c);
         if ((rc = hip_check(hipGetLastError(), "k_sw launch"))) return fail(rc);
@@ -841,7 +1050,10 @@ extern "C" int hclib_hip_sw_band_rows(hclib_hip_sw_band_t *h, int i0, int i1, co
     // each granule wait ends (rows above i0 finished in an earlier launch)
     int grid = i1 - i0;
     if (grid > h->grid_cap) grid = h->grid_cap;
-    if (c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
+    const char *sched = getenv("HCLIB_HIP_SW_SCHED");
+    if (sw_band_ok(c.th) && !(sched && !strcmp(sched, "rows1")))
+        hipLaunchKernelGGL(k_sw_band_rows, dim3(grid), dim3(c.th), sw_band_lds_bytes(c.th / 64), (hipStream_t)stream, c);
+    else if (c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
     else hipLaunchKernelGGL(k_sw_rows<false>, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
     return hip_check(hipGetLastError(), "k_sw_rows (band) launch");
 }
