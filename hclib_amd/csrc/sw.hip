@@ -57,6 +57,7 @@ struct SwCtx {
     int progressive;  // row schedule: chunked bottom-row hand-off
     const int *left_in;  // [nth*th]
     int *right_out;      // [nth*th]
+    int form;            // multi-wave bands: 10 * skew + hand-off steps / 16
 };
 
 // alignment_score_matrix (smith_waterman.cpp:36-43) row for s2 code a, plus
@@ -548,49 +549,80 @@ __global__ __launch_bounds__(64) void k_sw_rows(SwCtx c) {
 // wave above through an LDS ring (ring w + 1 = wave w's bottom row, written
 // by its lane 63 every step). Wave 0's ring is filled from the up tile row's
 // granules (or the boundary row); wave NW-1 publishes its ring as the tile
-// row's granules. Flow control: prod[w] = columns of ring w written,
-// cons[w] = columns of ring w read, both per 64-column chunk. NW waves run
-// on the CU's 4 SIMDs at once instead of one wave per tile row.
+// row's granules. Hand-offs every kSwSub steps: prod[w] = columns of ring w
+// written, cons[w] = columns of ring w read, so wave w + 1 runs 64 + kSwSub
+// steps behind wave w. NW waves run on the CU's 4 SIMDs at once instead of
+// one wave per tile row.
 constexpr int kSwRing = 512;  // columns per inter-wave ring (+1 wrap slot)
 constexpr int kSwRingStride = kSwRing + 4;
+constexpr int kSwSub = 16;    // steps per hand-off
 
 __host__ __device__ inline size_t sw_band_lds_bytes(int nw) {
     return (size_t)(nw + 1) * kSwRingStride * 4  // rings
            + (size_t)nw * 128 * 4                 // per-wave dummy slots (lanes 0..62's ring writes)
-           + (size_t)nw * 1024                    // per-wave code rings: 4 byte-shifted copies, double-mapped
+           + (size_t)nw * 2048                    // per-wave code rings: 4 byte-shifted copies, double-mapped
            + 2 * 64 * 4;                          // prod / cons words
 }
 
-// the multi-wave kernel's shape: 64-row bands, 1..16 waves per tile row
-inline bool sw_band_ok(int th) { return th % 64 == 0 && th / 64 >= 1 && th / 64 <= 16; }
-
-__device__ __forceinline__ int lds_ld_acq(const int *p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+// the multi-wave kernel's shape: 64-row bands, 1..14 compute waves per tile
+// row (+ the ingress and egress waves)
+inline bool sw_band_ok(int th) { return th % 64 == 0 && th / 64 >= 1 && th / 64 <= 14; }
+// tile rows per workgroup: as many as 14 compute waves hold (fewer hand-offs
+// through global memory), HCLIB_HIP_SW_ROWS_PER_WG overrides
+inline int sw_band_rows_per_wg(int th) {
+    const int bpt = th / 64, most = 14 / bpt;
+    int k = env_int("HCLIB_HIP_SW_ROWS_PER_WG", 1);
+    return k < 1 ? 1 : (k > most ? most : k);
 }
-__device__ __forceinline__ void lds_st_rel(int *p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+
+// Flags between the waves of a workgroup. The LDS performs one wave's DS
+// operations in issue order, so a flag stored after the ring data is seen
+// after that data by any wave that reads the flag first and the data next;
+// only the compiler must keep the program order (no memory fence needed,
+// and none that would also wait for the wave's global loads and stores).
+// (The casts keep these DS operations: a volatile or atomic access through
+// a generic pointer becomes a FLAT one, which waits for the wave's global
+// memory traffic as well.)
+typedef __attribute__((address_space(3))) int lds_i32;
+__device__ __forceinline__ int lds_flag_ld(const int *p) {
+    asm volatile("" ::: "memory");
+    const int v = __hip_atomic_load((const lds_i32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    return __builtin_amdgcn_readfirstlane(v);  // wave-uniform: scalar branches
+}
+__device__ __forceinline__ void lds_flag_st(int *p, int v) {
+    asm volatile("" ::: "memory");
+    __hip_atomic_store((lds_i32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
 }
 
-// 64 steps of one wave's band from step s0. top4 = ring slots of columns
-// s0 .. s0 + 63 (lane-uniform, 16-byte aligned), code4 = this lane's
-// aligned code words for columns s0 - lane .. s0 - lane + 63 (4 codes each),
-// wb = this lane's write base (lane 63: the out ring's slot of column
-// s0 - 63; other lanes: their dummy slots). G-space cells (see sw_tile).
+// K steps of one wave's band from step s with skew S: lane L computes
+// column s - S L at step s, so the cell above (lane L-1's, one column
+// back... the same column) was computed S steps earlier. With S = 2 the DPP
+// shift that brings it over leaves the step's dependency chain (it moves a
+// value one step old), so a step costs one dependent max3 instead of a
+// max3 and a DPP; the price is a band ramp of 126 steps instead of 63.
+// top4 = ring slots of columns s .. s + K - 1 (lane-uniform, 16-byte
+// aligned), code4 = this lane's aligned code words for columns s - S lane ..
+// (4 codes each), wb = this lane's write slot for step s (lane 63: the out
+// ring's slot of column s - 63 S; other lanes: their dummy slots). G-space
+// cells (see sw_tile). left = h one step back, o2 = h two steps back (S = 2).
 // Operands of 4 steps are read two groups ahead, in program order before the
-// previous group's ring writes (LDS completes a wave's operations in order).
-template <bool MASK>
-__device__ __forceinline__ void sw_band_chunk(int s0, int ncols, const int *top4, const uint32_t *code4, int *wb,
-                                              uint32_t mrow, int &left, int &diag, int &out) {
+// previous group's ring writes.
+template <bool MASK, int S, int K>
+__device__ __forceinline__ void sw_band_sub(int s, int ncols, const int *top4, const uint32_t *code4, int *wb,
+                                            uint32_t mrow, int &left, int &diag, int &o2) {
+    constexpr int G = K / 4;
     const int lane = lane_id();
     int4 tn = *(const int4 *)top4, tn2 = *(const int4 *)(top4 + 4);
     uint32_t cn = code4[0], cn2 = code4[1];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
+    for (int m = 0; m < G; ++m) {
         const int4 tc = tn;
         const uint32_t cc = cn;
         tn = tn2;
         cn = cn2;
-        if (m < 14) {
+        if (m + 2 < G) {
             tn2 = *(const int4 *)(top4 + 4 * (m + 2));
             cn2 = code4[m + 2];
         }
@@ -600,142 +632,317 @@ __device__ __forceinline__ void sw_band_chunk(int s0, int ncols, const int *top4
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int k = 4 * m + j;
-            const int up = __builtin_amdgcn_update_dpp(tv[j], out, 0x138, 0xf, 0xf, false);
+            const int up = __builtin_amdgcn_update_dpp(tv[j], S == 1 ? left : o2, 0x138, 0xf, 0xf, false);
             const int d = diag + (int)(int8_t)(sc >> (8 * j));
             const int a = left > up ? left : up;
             int h = a > d ? a : d;
             if (MASK) {
-                const bool v = (unsigned)(s0 + k - lane) < (unsigned)ncols;
+                const bool v = (unsigned)(s + k - S * lane) < (unsigned)ncols;
                 h = v ? h : left;
                 diag = v ? up : diag;
             } else {
                 diag = up;
             }
+            if (S == 2) o2 = left;
             left = h;
-            out = h;
             wb[k] = h;
         }
     }
 }
 
+// Wait for an LDS flag. The device error word and the clock are looked at
+// only every 64 polls: a global load here would wait for all of the wave's
+// outstanding global memory operations.
 __device__ bool sw_band_spin(const SwCtx &c, const int *flag, int want, unsigned long long t0) {
-    while (lds_ld_acq(flag) < want) {
-        if (ld_agent(c.err)) return false;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
-            if (lane_id() == 0) dev_error(c.err, kErrSpinTimeout);
-            return false;
-        }
+    want = __builtin_amdgcn_readfirstlane(want);
+    for (uint32_t n = 1; lds_flag_ld(flag) < want; ++n) {
         __builtin_amdgcn_s_sleep(1);
+        if ((n & 63) == 0) {
+            if (ld_agent(c.err)) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
+                if (lane_id() == 0) dev_error(c.err, kErrSpinTimeout);
+                return false;
+            }
+        }
     }
     return true;
 }
 
 // One wave's band of tile row i over the band's columns (matrix columns
 // C0 + 1 .. C0 + ncols, C0 = j0 * tw). Returns false on a device error.
-__device__ bool sw_band_row(const SwCtx &c, int i, int w, int nw, int *rings, int *dummy, uint8_t *code_rings,
-                            int *prod, int *cons) {
+// Diagnostic build only (HX_STAMPS): ph[0] compute, [1] waiting for the
+// top row, [2] waiting for ring space, [3] staging + publishing (cycles).
+// What one workgroup's bands compute: rows R0 + 1 .. R0 + 64 nb (nb bands)
+// over columns C0 + 1 .. C0 + ncols, from a top row, a left column and a
+// corner, to a bottom row and a right column. The row schedule hands top and
+// bottom rows between workgroups as tagged granules (polled); a tile task of
+// the promise DAG reads and writes the reference's plain arrays (its inputs
+// are complete before it runs).
+struct SwBand {
+    int R0, C0, ncols, nb;
+    const int *leftcol;  // H(R0 + 1 + k, C0), k < 64 nb; null when C0 == 0
+    int corner_h;        // H(R0, C0)
+    int *rightcol;       // H(R0 + 1 + k, C0 + ncols) out, or null
+    const unsigned long long *gin;  // top row as tagged granules, or
+    const int *hin;                 // as plain H; both null: the boundary row (R0 == 0)
+    unsigned long long *gout;       // bottom row as tagged granules, or
+    int *hout;                      // as plain H, with
+    int *corner_out;                //   its last value here (may be null)
+};
+
+// The workgroup's ingress wave: moves the top row into ring 0 and publishes
+// prod[0], so that no compute wave ever waits on a global load. Granules are
+// polled 128 columns per round trip (two loads per lane in flight) and the
+// longest ready prefix is published.
+__device__ bool sw_band_ingress(const SwCtx &c, const SwBand &B, int *ring0, int *prod, int *cons) {
     const int lane = lane_id();
-    const int th = c.th, C0 = c.j0 * c.tw, ncols = (c.j1 - c.j0) * c.tw;
-    const size_t gstride = (size_t)c.ntw * c.tw;  // granules per tile row
-    int *ring_in = rings + (size_t)w * kSwRingStride, *ring_out = ring_in + kSwRingStride;
-    uint8_t *cr = code_rings + w * 1024;
-    const int r = i * th + w * 64 + lane + 1;  // this lane's matrix row
-    const uint32_t mrow = sw_row2(c.s2[r - 1]);
-    // G at (r, C0) and (r - 1, C0): the band's left column
-    auto left_h = [&](int row) {
-        return row == 0 ? -C0 : (c.j0 == 0 ? -row : ld_agent(&c.left_in[row - 1]));
-    };
-    int left = left_h(r) + r + C0;
-    int diag = left_h(r - 1) + (r - 1) + C0;
-    int out = 0;
-    int *wbase = lane == 63 ? ring_out : dummy + w * 128 + lane;
-    const int8_t *s1 = c.s1 + C0;
-    int code_nx = lane < ncols ? s1[lane] - 1 : 0;  // code of column s0 + lane
-    unsigned long long pf = 0;                      // wave 0: granule of column s0 + lane
-    const unsigned long long *gup = c.gbot + (size_t)(i - 1) * gstride + C0;
-    if (w == 0 && i > 0 && lane < ncols) pf = ld_agent(&gup[lane]);
+    const int ncols = B.ncols;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (int s0 = 0; s0 < ncols + 63; s0 += 64) {
-        const int slot = s0 & (kSwRing - 1);
-        // (a) this chunk's top row: columns s0 .. s0 + 63 in ring_in
-        if (w == 0) {
-            const int cc = s0 + lane;
-            const bool need = i > 0 && cc < ncols;
-            while (!__all(!need || (pf >> 32) == 1ull)) {
+    int next = 0;
+    for (uint32_t n = 1; next < ncols; ++n) {
+        if (next + 128 - kSwRing > 0 && !sw_band_spin(c, &cons[0], next + 128 - kSwRing, t0)) return false;
+        const int x0 = next + lane, x1 = x0 + 64;
+        const int xa = x0 < ncols ? x0 : ncols - 1, xb = x1 < ncols ? x1 : ncols - 1;
+        const int ga = B.R0 + (B.C0 + x0 + 1), gb = B.R0 + (B.C0 + x1 + 1);  // H -> G
+        int m;
+        if (B.gin) {
+            // every other poll reads through this XCD's L2 (an sc0 load): the
+            // up workgroup normally runs on the same XCD (see k_sw_band_rows),
+            // whose L2 holds its write-through stores at once; the agent-scope
+            // polls in between keep the hand-off correct on any placement
+            unsigned long long a, b;
+            if (n & 1) {
+                a = __hip_atomic_load(&B.gin[xa], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                b = __hip_atomic_load(&B.gin[xb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                a = ld_agent(&B.gin[xa]);
+                b = ld_agent(&B.gin[xb]);
+            }
+            const bool ra = (a >> 32) == 1ull || x0 >= ncols, rb = (b >> 32) == 1ull || x1 >= ncols;
+            const unsigned long long ba = __ballot(ra), bb = __ballot(rb);
+            m = ~ba ? __builtin_ctzll(~ba) : (~bb ? 64 + __builtin_ctzll(~bb) : 128);
+            if (lane < m) ring0[x0 & (kSwRing - 1)] = (int)(uint32_t)a + ga;
+            if (lane + 64 < m) ring0[x1 & (kSwRing - 1)] = (int)(uint32_t)b + gb;
+        } else {
+            // complete inputs (a DAG tile's) or the boundary row, H(0, c) = -c
+            ring0[x0 & (kSwRing - 1)] = B.hin ? ld_agent(&B.hin[xa]) + ga : 0;
+            ring0[x1 & (kSwRing - 1)] = B.hin ? ld_agent(&B.hin[xb]) + gb : 0;
+            m = 128;
+        }
+        if (m > 0) {
+            next = next + m < ncols ? next + m : ncols;
+            if (lane == 0) lds_flag_st(&prod[0], next);
+        } else {
+            __builtin_amdgcn_s_sleep(2);
+            if ((n & 255) == 0) {
+                if (ld_agent(c.err)) return false;
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
                     if (lane == 0) dev_error(c.err, kErrSpinTimeout);
                     return false;
                 }
-                __builtin_amdgcn_s_sleep(1);
-                if (need) pf = ld_agent(&gup[cc]);
-            }
-            // tile row 0: G of the boundary row is 0 (H = -col)
-            ring_in[slot + lane] = need ? (int)(uint32_t)pf + i * th + (C0 + cc + 1) : 0;
-            if (i > 0 && cc + 64 < ncols) pf = ld_agent(&gup[cc + 64]);
-        } else {
-            const int want = s0 + 64 < ncols ? s0 + 64 : ncols;
-            if (!sw_band_spin(c, &prod[w], want, t0)) return false;
-        }
-        // (b) ring_out's slots for columns s0 - 63 .. s0 are free
-        if (w + 1 < nw && s0 + 1 - kSwRing > 0)
-            if (!sw_band_spin(c, &cons[w + 1], s0 + 1 - kSwRing, t0)) return false;
-        // (c) codes of columns s0 .. s0 + 63: copy o holds column x at byte
-        // (x + o) mod 128 (and + 128), so lane L reads aligned words from
-        // copy L mod 4
-        {
-#pragma unroll
-            for (int o = 0; o < 4; ++o) {
-                const int q = (s0 + lane + o) & 127;
-                cr[o * 256 + q] = (uint8_t)code_nx;
-                cr[o * 256 + q + 128] = (uint8_t)code_nx;
-            }
-            const int cn = s0 + 64 + lane;
-            code_nx = cn < ncols ? s1[cn] - 1 : 0;
-        }
-        const uint32_t *cb = (const uint32_t *)(cr + (lane & 3) * 256 + ((s0 - lane + (lane & 3)) & 127));
-        int *wb = wbase + (lane == 63 ? ((s0 - 63) & (kSwRing - 1)) : 0);
-        if (s0 >= 64 && s0 + 64 <= ncols)
-            sw_band_chunk<false>(s0, ncols, ring_in + slot, cb, wb, mrow, left, diag, out);
-        else
-            sw_band_chunk<true>(s0, ncols, ring_in + slot, cb, wb, mrow, left, diag, out);
-        // (e) lane 63's last column (s0) also at its own slot (the wrap slot fix)
-        if (lane == 63) ring_out[slot] = left;
-        // (f) publish: columns < s0 + 1 of ring_out, columns < s0 + 64 of ring_in read
-        if (lane == 0) {
-            lds_st_rel(&prod[w + 1], s0 + 1 < ncols ? s0 + 1 : ncols);
-            lds_st_rel(&cons[w], s0 + 64);
-        }
-        // (h) the last wave hands its bottom row to the next tile row
-        if (w == nw - 1) {
-            const int cc = s0 - 63 + lane;
-            if (cc >= 0 && cc < ncols) {
-                const int h = ring_out[cc & (kSwRing - 1)] - (i + 1) * th - (C0 + cc + 1);
-                st_agent(&c.gbot[(size_t)i * gstride + C0 + cc], (1ull << 32) | (unsigned long long)(uint32_t)h);
             }
         }
     }
-    if (c.right_out) c.right_out[r - 1] = left - r - (C0 + ncols);
     return true;
 }
 
+// The workgroup's egress wave: stores the last band's bottom row (ring nb)
+// as granules or plain H, up to 64 columns per batch, and publishes
+// cons[nb]; the compute waves issue no global stores but the right column.
+__device__ bool sw_band_egress(const SwCtx &c, const SwBand &B, int *ring, int *prod, int *cons) {
+    const int lane = lane_id();
+    const int ncols = B.ncols, nb = B.nb, Rb = B.R0 + 64 * nb;  // matrix row of the bottom row
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int next = 0;
+    while (next < ncols) {
+        const int want = next + kSwSub < ncols ? next + kSwSub : ncols;
+        if (!sw_band_spin(c, &prod[nb], want, t0)) return false;
+        int avail = lds_flag_ld(&prod[nb]);
+        avail = avail < next + 64 ? avail : next + 64;
+        const int x = next + lane;
+        if (x < avail) {
+            const int h = ring[x & (kSwRing - 1)] - Rb - (B.C0 + x + 1);
+            if (B.gout) st_agent(&B.gout[x], (1ull << 32) | (unsigned long long)(uint32_t)h);
+            else st_agent(&B.hout[x], h);
+            if (B.corner_out && x == ncols - 1) st_agent(B.corner_out, h);
+        }
+        next = avail;
+        if (lane == 0) lds_flag_st(&cons[nb], next);
+    }
+    return true;
+}
+
+// One wave's band (band w of the workgroup's nb) over the band's columns,
+// skew S, hand-offs every K steps. Returns false on a device error.
+// Diagnostic build only (HX_STAMPS): ph[0] compute, [1] waiting for the top
+// row, [2] waiting for ring space + staging codes, [3] publishing (cycles).
+template <int S, int K>
+__device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, int *dummy, uint8_t *code_rings,
+                            int *prod, int *cons, unsigned long long *ph, bool stamp_first) {
+    constexpr int D = 63 * S;        // lane 63's lag in steps
+    constexpr int CR = S == 1 ? 128 : 256;  // code ring columns (needs D + 64)
+    unsigned long long ts = sw_stamp();
+    auto phase = [&](int k) {
+        if (HX_STAMPS) {
+            const unsigned long long now = sw_stamp();
+            ph[k] += now - ts;
+            ts = now;
+        }
+    };
+    const int lane = lane_id();
+    const int C0 = B.C0, ncols = B.ncols;
+    int *ring_in = rings + (size_t)w * kSwRingStride, *ring_out = ring_in + kSwRingStride;
+    uint8_t *cr = code_rings + w * 2048;
+    const int r = B.R0 + w * 64 + lane + 1;  // this lane's matrix row
+    const uint32_t mrow = sw_row2(c.s2[r - 1]);
+    // G at (r, C0) and (r - 1, C0): the band's left column
+    auto left_h = [&](int row) {
+        return C0 == 0 ? -row : (row == B.R0 ? B.corner_h : ld_agent(&B.leftcol[row - B.R0 - 1]));
+    };
+    int left = left_h(r) + r + C0;
+    int diag = left_h(r - 1) + (r - 1) + C0;
+    int o2 = left;
+    int *wbase = lane == 63 ? ring_out : dummy + w * 128 + lane;
+    const int8_t *s1 = c.s1 + C0;
+    // s1 code (1..4) of column x; loads clamped to the band, never predicated,
+    // so that nothing waits for them before their use
+    auto code_at = [&](int x) { return s1[x < ncols ? x : ncols - 1]; };
+    // copy o holds column x's code - 1 at byte (x + o) mod CR (and + CR), so
+    // lane L reads aligned words from copy (S L) mod 4
+    auto stage_codes = [&](int x, int code) {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+            const int q = (x + o) & (CR - 1);
+            cr[o * 2 * CR + q] = (uint8_t)(code - 1);
+            cr[o * 2 * CR + q + CR] = (uint8_t)(code - 1);
+        }
+    };
+    stage_codes(lane, code_at(lane));
+    const int cofs = (S * lane) & 3;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    for (int s0 = 0; ok && s0 < ncols + D; s0 += 64) {
+        const int slot = s0 & (kSwRing - 1);
+        // ring_out's slots for columns s0 - D .. s0 + 63 - D are free
+        if (s0 + 64 - D - kSwRing > 0 && !sw_band_spin(c, &cons[w + 1], s0 + 64 - D - kSwRing, t0)) {
+            ok = false;
+            break;
+        }
+        // the next chunk's codes (staged after this chunk's last read)
+        const int craw = code_at(s0 + 64 + lane);
+        const uint32_t *cb = (const uint32_t *)(cr + cofs * 2 * CR + ((s0 - S * lane + cofs) & (CR - 1)));
+        int *wb = wbase + (lane == 63 ? ((s0 - D) & (kSwRing - 1)) : 0);
+        const bool full = s0 >= D && s0 + 64 <= ncols;
+        phase(2);
+#pragma unroll
+        for (int q = 0; q < 64 / K; ++q) {
+            const int s = s0 + q * K;
+            // this hand-off's top row: columns s .. s + K - 1 of ring_in
+            if (!sw_band_spin(c, &prod[w], s + K < ncols ? s + K : ncols, t0)) {
+                ok = false;
+                break;
+            }
+            if (HX_STAMPS && s == 0 && w == 0 && lane == 0 && stamp_first) {
+                // first input of the tile row (global clock): rows' start spacing
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                if (B.R0 == c.i0 * c.th) st_agent(&c.stats[21], now);
+                if (B.R0 + 64 * B.nb == c.i1 * c.th) st_agent(&c.stats[20], now);
+            }
+            phase(1);
+            if (full)
+                sw_band_sub<false, S, K>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mrow, left,
+                                         diag, o2);
+            else
+                sw_band_sub<true, S, K>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mrow, left,
+                                        diag, o2);
+            phase(0);
+            // lane 63's last S columns of the chunk may have gone past the
+            // ring's end (wrap slots): they are also stored at their own slots
+            if (q == 64 / K - 1 && lane == 63) {
+                ring_out[(s0 + 63 - D) & (kSwRing - 1)] = left;
+                if (S == 2) ring_out[(s0 + 62 - D) & (kSwRing - 1)] = o2;
+            }
+            // publish: ring_out holds columns < s + K - D, ring_in's columns
+            // < s + K are read
+            if (lane == 0) {
+                const int pc = s + K - D;
+                lds_flag_st(&prod[w + 1], pc < 0 ? 0 : (pc < ncols ? pc : ncols));
+                lds_flag_st(&cons[w], s + K);
+            }
+            phase(3);
+        }
+        stage_codes(s0 + 64 + lane, craw);
+    }
+    if (HX_STAMPS && stamp_first && w == B.nb - 1 && lane == 0 && B.R0 + 64 * B.nb == c.i1 * c.th)
+        st_agent(&c.stats[22], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (ok && B.rightcol) st_agent(&B.rightcol[r - B.R0 - 1], left - r - (C0 + ncols));
+    return ok;
+}
+
+// the (skew, hand-off) forms: HCLIB_HIP_SW_FORM = 10 S + K / 16
+__device__ __forceinline__ bool sw_band_row_any(int form, const SwCtx &c, const SwBand &B, int w, int *rings,
+                                                int *dummy, uint8_t *code_rings, int *prod, int *cons,
+                                                unsigned long long *ph, bool stamp_first) {
+    switch (form) {
+        case 11: return sw_band_row<1, 16>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 12: return sw_band_row<1, 32>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 21: return sw_band_row<2, 16>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        default: return sw_band_row<2, 32>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+    }
+}
+
+// A workgroup runs k consecutive tile rows (k * th / 64 compute waves, then
+// the ingress and the egress wave): only every k-th tile row boundary
+// crosses workgroups through global memory.
 __global__ __launch_bounds__(1024) void k_sw_band_rows(SwCtx c) {
     extern __shared__ __attribute__((aligned(16))) int sw_lds[];
-    const int nw = (int)(blockDim.x >> 6), w = (int)(threadIdx.x >> 6);
+    const int nwave = (int)(blockDim.x >> 6) - 2, w = (int)(threadIdx.x >> 6);
+    const int bpt = c.th / 64, k = nwave / bpt;
     int *rings = sw_lds;
-    int *dummy = rings + (size_t)(nw + 1) * kSwRingStride;
-    uint8_t *code_rings = (uint8_t *)(dummy + nw * 128);
-    int *prod = (int *)(code_rings + nw * 1024), *cons = prod + 64;
+    int *dummy = rings + (size_t)(nwave + 1) * kSwRingStride;
+    uint8_t *code_rings = (uint8_t *)(dummy + nwave * 128);
+    int *prod = (int *)(code_rings + nwave * 2048), *cons = prod + 64;
+    const size_t gstride = (size_t)c.ntw * c.tw;  // granules per tile row
     bool ok = true;
     unsigned long long ntile = 0;
-    for (int i = c.i0 + (int)blockIdx.x; i < c.i1; i += gridDim.x) {
+    unsigned long long ph[4] = {0, 0, 0, 0};
+    // blocks of k tile rows; with the grid a multiple of the 8 XCDs, block
+    // positions are dealt so that consecutive blocks run on one XCD (the
+    // dispatcher places workgroup b on XCD b mod 8 — for speed only: every
+    // hand-off is correct on any placement). Each workgroup takes its blocks
+    // in increasing order and all are resident, so every wait ends.
+    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    const int p0 = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
+    for (int i = c.i0 + p0 * k; i < c.i1; i += G * k) {
+        const int kk = k < c.i1 - i ? k : c.i1 - i;  // tile rows of this block
+        SwBand B;
+        B.R0 = i * c.th;
+        B.C0 = c.j0 * c.tw;
+        B.ncols = (c.j1 - c.j0) * c.tw;
+        B.nb = kk * bpt;
+        B.leftcol = c.j0 > 0 ? c.left_in + B.R0 : nullptr;
+        B.corner_h = B.R0 == 0 ? -B.C0 : (c.j0 == 0 ? -B.R0 : (c.j0 > 0 ? ld_agent(&c.left_in[B.R0 - 1]) : 0));
+        B.rightcol = c.right_out ? c.right_out + B.R0 : nullptr;
+        B.gin = i > 0 ? c.gbot + (size_t)(i - 1) * gstride + B.C0 : nullptr;
+        B.hin = nullptr;
+        B.gout = c.gbot + (size_t)(i + kk - 1) * gstride + B.C0;
+        B.hout = nullptr;
+        B.corner_out = nullptr;
         if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod[0..63], cons[0..63]
         __syncthreads();
-        ok = sw_band_row(c, i, w, nw, rings, dummy, code_rings, prod, cons);
+        if (w == nwave)
+            ok = sw_band_ingress(c, B, rings, prod, cons);
+        else if (w == nwave + 1)
+            ok = sw_band_egress(c, B, rings + (size_t)B.nb * kSwRingStride, prod, cons);
+        else if (w < B.nb)
+            ok = sw_band_row_any(c.form, c, B, w, rings, dummy, code_rings, prod, cons, ph, true);
         vm_drain();
         if (__syncthreads_or(!ok)) break;  // every wave leaves together
-        ntile += (unsigned long long)(c.j1 - c.j0);
+        ntile += (unsigned long long)(c.j1 - c.j0) * kk;
     }
     if (threadIdx.x == 0) add_agent(&c.stats[0], ntile);
+    if (HX_STAMPS && lane_id() == 0 && w < 4)  // per compute wave (first four)
+        for (int q = 0; q < 4; ++q) add_agent(&c.stats[4 + 4 * w + q], ph[q]);
 }
 
 // The generic device promise DAG (include/hclib_hip/hx_dag.h) driving the
@@ -764,6 +971,54 @@ struct SwDagKind {
 
 __global__ __launch_bounds__(64) void k_sw_dag(SwCtx c, DagView v) {
     run_dag_worker<SwDagKind>(c, v);
+}
+
+// The same tile program with every tile task run by a workgroup: th / 64
+// compute waves (one 64-row band each, chained through LDS rings as in the
+// row schedule) plus the ingress wave (the up tile's bottom row into ring 0)
+// and the egress wave (the bottom row and corner out); the tile's three
+// promises are put by wave 0 once every wave's stores are drained.
+struct SwDagWgKind {
+    using Ctx = SwCtx;
+    __device__ static bool run_group(const SwCtx &c, uint32_t t, const uint32_t *, int wave) {
+        extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+        const int nw = c.th / 64;
+        int *rings = sw_lds;
+        int *dummy = rings + (size_t)(nw + 1) * kSwRingStride;
+        uint8_t *code_rings = (uint8_t *)(dummy + nw * 128);
+        int *prod = (int *)(code_rings + nw * 2048), *cons = prod + 64;
+        const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
+        SwBand B;
+        B.R0 = i * c.th;
+        B.C0 = j * c.tw;
+        B.ncols = c.tw;
+        B.nb = nw;
+        B.leftcol = j > 0 ? c.right + (size_t)(t - 1) * c.th : nullptr;
+        B.corner_h = B.R0 == 0 ? -B.C0 : (j == 0 ? -B.R0 : ld_agent(&c.corner[t - (uint32_t)c.ntw - 1]));
+        B.rightcol = c.right + (size_t)t * c.th;
+        B.gin = nullptr;
+        B.hin = i > 0 ? c.bottom + (size_t)(t - (uint32_t)c.ntw) * c.tw : nullptr;
+        B.gout = nullptr;
+        B.hout = c.bottom + (size_t)t * c.tw;
+        B.corner_out = c.corner + t;
+        if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod[0..63], cons[0..63]
+        __syncthreads();
+        unsigned long long ph[4] = {0, 0, 0, 0};
+        if (wave == nw) return sw_band_ingress(c, B, rings, prod, cons);
+        if (wave == nw + 1) return sw_band_egress(c, B, rings + (size_t)nw * kSwRingStride, prod, cons);
+        return sw_band_row_any(c.form, c, B, wave, rings, dummy, code_rings, prod, cons, ph, false);
+    }
+    // right column, bottom row, corner (:212-226): one release for all three
+    __device__ static void put(const SwCtx &c, DagWave &w, uint32_t t) {
+        const uint32_t ps[3] = {3u * t + 0u, 3u * t + 1u, 3u * t + 2u};
+        const unsigned long long ds[3] = {0ull, 0ull, (unsigned long long)(uint32_t)ld_agent(&c.corner[t])};
+        dag_put_n<3>(w, ps, ds);
+    }
+};
+
+__global__ __launch_bounds__(1024) void k_sw_dag_wg(SwCtx c, DagView v) {
+    __shared__ uint32_t task_slot;
+    run_dag_group<SwDagWgKind>(c, v, &task_slot);
 }
 
 __global__ void k_sw_init(uint32_t *deps, uint32_t *ready, int ntw, int nth) {
@@ -806,7 +1061,8 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     const bool rows = !(sched && (!strcmp(sched, "queue") || dag)) && rows_lds <= 64 * 1024;
     // multi-wave tile rows (th / 64 waves per workgroup) unless "rows1" asks
     // for the one-wave-per-tile-row kernel
-    const bool band = rows && sw_band_ok(th) && !(sched && !strcmp(sched, "rows1"));
+    const bool band_shape = sw_band_ok(th) && tw <= 65536;
+    const bool band = rows && band_shape && !(sched && !strcmp(sched, "rows1"));
     const size_t nt = ntw * nth;
     const size_t b_s1 = ntw * tw, b_s2 = nth * th;
     const size_t b_bot = rows ? 0 : nt * tw * 4, b_right = rows ? 0 : nt * th * 4, b_c = nt * 4,
@@ -846,6 +1102,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     c.left_in = nullptr;
     c.right_out = nullptr;
     c.progressive = env_int("HCLIB_HIP_SW_PROGRESSIVE", 1);
+    c.form = env_int("HCLIB_HIP_SW_FORM", 12);
     int rc = HCLIB_HIP_OK;
     auto fail = [&](int r) { (void)hipFree(d); return r; };
     if ((rc = hip_check(hipMemcpyAsync((void *)c.s1, s1, b_s1, hipMemcpyHostToDevice, m.stream), "copy s1"))) return fail(rc);
@@ -890,19 +1147,31 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
             if (i > 0 && j > 0) ids.push_back((uint32_t)(3 * (t - ntw - 1) + 2));
             off[t + 1] = (uint32_t)ids.size();
         }
+        // tile tasks on workgroups of th / 64 + 2 waves where the band
+        // kernel applies (HCLIB_HIP_SW_DAG_WAVE=1: one wave per tile)
+        const bool wg = band_shape && env_int("HCLIB_HIP_SW_DAG_WAVE", 0) == 0;
         hclib_hip_dag_launch_t L;
         if ((rc = hclib_hip_dag_begin((uint32_t)nt, (uint32_t)(3 * nt), 0, nullptr, off.data(), ids.data(), nullptr,
-                                      nullptr, wpc, c.spin_ms, &L)))
+                                      nullptr, wg ? 1 : wpc, c.spin_ms, &L)))
             return fail(rc);
-        hipLaunchKernelGGL(k_sw_dag, dim3(L.grid), dim3(64), lds, m.stream, c, *(const DagView *)L.view);
+        if (wg) {
+            const size_t blds = sw_band_lds_bytes(th / 64);
+            if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_wg,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
+            hipLaunchKernelGGL(k_sw_dag_wg, dim3(L.grid), dim3(th + 128), blds, m.stream, c, *(const DagView *)L.view);
+        } else {
+            hipLaunchKernelGGL(k_sw_dag, dim3(L.grid), dim3(64), lds, m.stream, c, *(const DagView *)L.view);
+        }
         if ((rc = hclib_hip_dag_end("hclib_hip_sw (dag)", nullptr, nullptr, &dst))) return fail(rc);
     } else {
         if ((rc = hip_check(hipEventRecord(m.ev0, m.stream), "event"))) return fail(rc);
         if (band) {
-            int g = (int)nth < m.num_cus ? (int)nth : m.num_cus;
-            if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_band_rows,
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(k_sw_band_rows, dim3(g), dim3(th), lds, m.stream, c);
+            const int k = sw_band_rows_per_wg(th), nblk = ((int)nth + k - 1) / k;
+            const int g = nblk < m.num_cus ? nblk : m.num_cus;
+            const size_t blds = sw_band_lds_bytes(k * (th / 64));
+            if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_band_rows,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
+            hipLaunchKernelGGL(k_sw_band_rows, dim3(g), dim3(k * th + 128), blds, m.stream, c);
         } else if (rows && c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), lds, m.stream, c);
         else if (rows) hipLaunchKernelGGL(k_sw_rows<false>, dim3(grid), dim3(64), lds, m.stream, c);
         else hipLaunchKernelGGL(k_sw, dim3(grid), dim3(64), lds, m.stream, c);
@@ -915,7 +1184,16 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     if ((rc = hip_check(hipStreamSynchronize(m.stream), "k_sw"))) return fail(rc);
     (void)hipMemcpy(&herr, c.err, 4, hipMemcpyDeviceToHost);
     (void)hipMemcpy(st, c.stats, sizeof(st), hipMemcpyDeviceToHost);
-    if (HX_STAMPS && st[0])
+    if (HX_STAMPS && band) {
+        unsigned long long t[23] = {0};
+        (void)hipMemcpy(t, c.stats, sizeof(t), hipMemcpyDeviceToHost);
+        for (int w = 0; w < 4 && w < th / 64; ++w)
+            fprintf(stderr, "sw band wave %d phases (cycles per row): compute %.0f wait-top %.0f wait-ring %.0f staging %.0f\n",
+                    w, (double)t[4 + 4 * w] / nth, (double)t[5 + 4 * w] / nth, (double)t[6 + 4 * w] / nth,
+                    (double)t[7 + 4 * w] / nth);
+        fprintf(stderr, "sw band: row start spacing %.3f us, last row %.3f us\n",
+                nth > 1 ? (double)(t[20] - t[21]) * 0.01 / (double)(nth - 1) : 0.0, (double)(t[22] - t[20]) * 0.01);
+    } else if (HX_STAMPS && st[0])
         fprintf(stderr, "sw phases (cycles/tile): inputs %.0f band-setup %.0f ramp-in %.0f steady %.0f ramp-out %.0f outputs %.0f\n",
                 (double)st[4] / st[0], (double)st[5] / st[0], (double)st[6] / st[0], (double)st[7] / st[0],
                 (double)st[8] / st[0], (double)st[9] / st[0]);
@@ -1018,6 +1296,7 @@ extern "C" int hclib_hip_sw_band_begin(const int8_t *s1, size_t n1, const int8_t
     c.j0 = j0;
     c.j1 = j1;
     c.progressive = env_int("HCLIB_HIP_SW_PROGRESSIVE", 1);
+    c.form = env_int("HCLIB_HIP_SW_FORM", 12);
     c.spin_ms = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     h->lds = lds;
     h->grid_cap = m.num_cus;
@@ -1051,8 +1330,14 @@ extern "C" int hclib_hip_sw_band_rows(hclib_hip_sw_band_t *h, int i0, int i1, co
     int grid = i1 - i0;
     if (grid > h->grid_cap) grid = h->grid_cap;
     const char *sched = getenv("HCLIB_HIP_SW_SCHED");
-    if (sw_band_ok(c.th) && !(sched && !strcmp(sched, "rows1")))
-        hipLaunchKernelGGL(k_sw_band_rows, dim3(grid), dim3(c.th), sw_band_lds_bytes(c.th / 64), (hipStream_t)stream, c);
+    if (sw_band_ok(c.th) && !(sched && !strcmp(sched, "rows1"))) {
+        const int k = sw_band_rows_per_wg(c.th), nblk = (i1 - i0 + k - 1) / k;
+        const int g = nblk < h->grid_cap ? nblk : h->grid_cap;
+        const size_t blds = sw_band_lds_bytes(k * (c.th / 64));
+        if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_band_rows,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
+        hipLaunchKernelGGL(k_sw_band_rows, dim3(g), dim3(k * c.th + 128), blds, (hipStream_t)stream, c);
+    }
     else if (c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
     else hipLaunchKernelGGL(k_sw_rows<false>, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
     return hip_check(hipGetLastError(), "k_sw_rows (band) launch");

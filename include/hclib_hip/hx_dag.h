@@ -136,12 +136,95 @@ __device__ __forceinline__ void dag_put(DagWave &w, uint32_t p, unsigned long lo
 }
 
 // Several puts of one task behind a single release (a tile that satisfies
-// its right-column, bottom-row and corner promises at once).
+// its right-column, bottom-row and corner promises at once), in three
+// memory round trips whatever N is: lane i < N publishes promise i (datum,
+// satisfied exchange, waiter range), then the lanes decrement the waiters of
+// all N promises together (each lane one waiter of the concatenated lists),
+// then the released tasks take ready-list slots (one kept, as dag_put_one).
+// Waiter lists longer than 64 in total fall back to one put at a time.
 template <int N>
 __device__ __forceinline__ void dag_put_n(DagWave &w, const uint32_t (&p)[N], const unsigned long long (&datum)[N]) {
+    static_assert(N >= 1 && N <= 64, "dag_put_n: 1..64 promises");
     release_agent();
+    const DagView &v = w.v;
+    const int lane = lane_id();
+    uint32_t my_p = 0, b = 0, e = 0, was = 0;
 #pragma unroll
-    for (int i = 0; i < N; ++i) dag_put_one(w, p[i], datum[i]);
+    for (int i = 0; i < N; ++i)
+        if (lane == i) my_p = p[i];
+    if (lane < N) {
+        unsigned long long d = 0;
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (lane == i) d = datum[i];
+        st_agent(&v.datum[my_p], d);
+        was = __hip_atomic_exchange(&v.satisfied[my_p], 1u, __ATOMIC_RELAXED, HX_AGENT);
+        b = v.waiter_off[my_p];
+        e = v.waiter_off[my_p + 1];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the data land before any release
+    if (__ballot(lane < N && was != 0)) {  // src/hclib-promise.c:206-207
+        if (lane == 0) dev_error(v.err, kErrDoublePut);
+        return;
+    }
+    // concatenated waiter lists: promise i's waiters at [pre_i, pre_i + n_i)
+    // (wave-uniform copies, read before any divergent branch)
+    uint32_t ub[N], un[N], upre[N], total = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        ub[i] = (uint32_t)__builtin_amdgcn_readlane((int)b, i);
+        un[i] = (uint32_t)__builtin_amdgcn_readlane((int)e, i) - ub[i];
+        upre[i] = total;
+        total += un[i];
+    }
+    if (total > 64) {  // long lists: promise by promise (already published)
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const uint32_t bi = ub[i], ei = ub[i] + un[i];
+            uint32_t rel = 0;
+            for (uint32_t k0 = bi; k0 < ei; k0 += 64) {
+                const uint32_t k = k0 + (uint32_t)lane;
+                if (k < ei) {
+                    const uint32_t c = v.waiters[k];
+                    if (add_agent(&v.deps[c], (uint32_t)-1) == 1u) {
+                        st_agent(&v.ready[add_agent(v.tail, 1u)], c);
+                        ++rel;
+                    }
+                }
+            }
+            w.puts += 1;
+            w.releases += (unsigned long long)wave_sum((int)rel);
+        }
+        return;
+    }
+    // lane k: waiter k of the concatenation
+    uint32_t idx = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if ((uint32_t)lane >= upre[i] && (uint32_t)lane < upre[i] + un[i]) idx = ub[i] + ((uint32_t)lane - upre[i]);
+    uint32_t t = kDagEmpty;
+    if ((uint32_t)lane < total) {
+        const uint32_t c = v.waiters[idx];
+        if (add_agent(&v.deps[c], (uint32_t)-1) == 1u) t = c;
+    }
+    uint32_t rel = 0;
+    const unsigned long long m = __ballot(t != kDagEmpty);
+    if (m && w.next == kDagEmpty) {  // keep one released task (see dag_put_one)
+        const int leader = __builtin_ctzll(m);
+        w.next = (uint32_t)__builtin_amdgcn_readlane((int)t, leader);
+        w.skip_lane = leader;
+        if (lane == leader) {
+            w.skip_pos = add_agent(v.tail, 1u);
+            t = kDagEmpty;
+            ++rel;
+        }
+    }
+    if (t != kDagEmpty) {
+        st_agent(&v.ready[add_agent(v.tail, 1u)], t);
+        ++rel;
+    }
+    w.puts += N;
+    w.releases += (unsigned long long)wave_sum((int)rel);
 }
 
 // Kind concept:
@@ -201,6 +284,78 @@ __device__ void run_dag_worker(const typename Kind::Ctx &ctx, const DagView &vie
         if (kept && lane == pend_lane) st_agent(&view.ready[pend_pos], kDagSkip);
     }
     if (lane == 0) {
+        add_agent(&view.stats[0], ran);
+        add_agent(&view.stats[1], w.puts);
+        add_agent(&view.stats[2], w.releases);
+    }
+}
+
+// Workgroup tasks: Kind::run_group(ctx, t, payload, wave) is a body every
+// wave of the workgroup enters (returns false after a device error); wave 0
+// takes the tickets, as run_dag_worker does, and after the body — every
+// wave's stores drained, then a barrier — runs Kind::put(ctx, DagWave&, t),
+// the task's puts. `slot` is one LDS word for the task id broadcast.
+// Concept additions: run_group and put as above.
+template <class Kind>
+__device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view, uint32_t *slot) {
+    DagWave w{view, 0, 0, kDagEmpty, 0, 0};
+    const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
+    unsigned long long ran = 0;
+    while (true) {
+        bool kept = false;
+        uint32_t pend_pos = 0;
+        int pend_lane = 0;
+        if (wave == 0) {
+            uint32_t t = kDagEmpty;
+            while (true) {
+                if (w.next != kDagEmpty) {
+                    t = w.next;
+                    w.next = kDagEmpty;
+                    kept = true;
+                    pend_pos = w.skip_pos;
+                    pend_lane = w.skip_lane;
+                    break;
+                }
+                uint32_t ticket = 0;
+                if (lane == 0) ticket = add_agent(view.head, 1u);
+                ticket = (uint32_t)__shfl((int)ticket, 0, 64);
+                t = kDagEmpty;
+                if (ticket >= view.ntasks) break;
+                if (lane == 0) {
+                    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                    while ((t = ld_agent(&view.ready[ticket])) == kDagEmpty) {
+                        if (ld_agent(view.err)) break;
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * view.spin_ms) {
+                            dev_error(view.err, kErrSpinTimeout);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                t = (uint32_t)__shfl((int)t, 0, 64);
+                if (t != kDagSkip) break;
+            }
+            if (t != kDagEmpty && t >= view.ntasks) {
+                if (lane == 0) dev_error(view.err, kErrBadTask);
+                t = kDagEmpty;
+            }
+            if (lane == 0) *slot = t;
+        }
+        __syncthreads();
+        const uint32_t t = *slot;
+        __syncthreads();  // the slot is rewritten only after this barrier
+        if (t == kDagEmpty) break;
+        acquire_agent();
+        const bool ok = Kind::run_group(ctx, t, view.payload + (size_t)t * view.payload_words, wave);
+        vm_drain();
+        if (__syncthreads_or(!ok)) break;
+        if (wave == 0) {
+            Kind::put(ctx, w, t);
+            if (kept && lane == pend_lane) st_agent(&view.ready[pend_pos], kDagSkip);
+        }
+        ++ran;
+    }
+    if (wave == 0 && lane == 0) {
         add_agent(&view.stats[0], ran);
         add_agent(&view.stats[1], w.puts);
         add_agent(&view.stats[2], w.releases);

@@ -275,14 +275,19 @@ def test_sw_random_vs_oracle():
         assert score == L.sw_score(s1, s2, tw, th)
 
 
-@pytest.mark.parametrize("sched", ["queue", "rows", "rows1", "dag"])
+@pytest.mark.parametrize("sched", ["queue", "rows", "rows1", "dag", "dag-wave"])
 def test_sw_both_schedules(golden, sched, monkeypatch):
     """The tile-counter schedule (device dependency counters + ready list),
     the row schedule (owner-computes tile rows, granule hand-offs; "rows" =
     th / 64 waves per tile row where th % 64 == 0, "rows1" = one wave) and the
     reference's own promise program on the generic device DAG (3 futures, 3
     puts per tile, include/hclib_hip/hx_dag.h) give the published scores and
-    the oracle's on ragged tile grids."""
+    the oracle's on ragged tile grids. The DAG's tile tasks run on workgroups
+    of th / 64 + 2 waves where th % 64 == 0 ("dag"), or one wave each
+    ("dag-wave")."""
+    if sched == "dag-wave":
+        sched = "dag"
+        monkeypatch.setenv("HCLIB_HIP_SW_DAG_WAVE", "1")
     monkeypatch.setenv("HCLIB_HIP_SW_SCHED", sched)
     g = golden("sw_goldens.json")["published"]["large"]
     s1, s2 = _sw_inputs("large")
@@ -320,19 +325,25 @@ def test_sw_row_schedule_hand_off_forms(golden, progressive, monkeypatch):
 
 
 @pytest.mark.parametrize("n1,n2,tw,th", [
-    (50, 300, 50, 64), (1000, 640, 30, 128), (4100, 1024, 4100, 512), (5000, 2048, 100, 1024),
+    (50, 300, 50, 64), (1000, 640, 30, 128), (4100, 1024, 4100, 512), (5000, 1792, 100, 896),
     (2048, 2048, 64, 64), (3333, 768, 1111, 256), (640, 192, 64, 192)])
 def test_sw_multiwave_tile_rows(n1, n2, tw, th, monkeypatch):
     """The multi-wave row kernel (one 64-row band per wave, th / 64 waves per
     tile row, inter-wave LDS rings): band widths below one 64-column chunk,
-    ragged last chunks, widths past the 512-column ring (wrap slot), 1..16
-    waves per workgroup — the oracle's score; and the one-wave kernel agrees."""
+    ragged last chunks, widths past the 512-column ring (wrap slot), 1..14
+    compute waves per workgroup — the oracle's score; the one-wave kernel agrees."""
     rng = np.random.default_rng(n1 * 7 + th)
     s1 = bytes(rng.integers(1, 5, n1, dtype=np.int8).tobytes())
     s2 = bytes(rng.integers(1, 5, n2, dtype=np.int8).tobytes())
     want = L.sw_score(s1, s2, tw, th)
-    score, st = H.sw(s1, s2, tw, th)
-    assert score == want and st["tiles"] == (n1 // tw) * (n2 // th)
+    # every (skew, hand-off) form: 10 * skew + hand-off steps / 16
+    for form in ("11", "12", "21", "22"):
+        monkeypatch.setenv("HCLIB_HIP_SW_FORM", form)
+        score, st = H.sw(s1, s2, tw, th)
+        assert score == want and st["tiles"] == (n1 // tw) * (n2 // th), form
+        monkeypatch.setenv("HCLIB_HIP_SW_SCHED", "dag")
+        assert H.sw(s1, s2, tw, th)[0] == want, ("dag", form)
+        monkeypatch.delenv("HCLIB_HIP_SW_SCHED")
     monkeypatch.setenv("HCLIB_HIP_SW_SCHED", "rows1")
     assert H.sw(s1, s2, tw, th)[0] == want
 
