@@ -114,15 +114,30 @@ def build_tests(verbose: bool = True) -> list:
             continue
         src = os.path.join(tdir, f)
         exe = os.path.join(out, f[:-4])
-        key = _hash([src] + _headers() + [LIB], CFLAGS)
+        # a HIP object of device kinds linked into a C program of its own
+        # (tests/c/<name>_main.c, compiled with gcc against include/hclib.h)
+        cmain = os.path.join(ROOT, "tests", "c", f[:-4] + "_main.c")
+        deps = [src] + ([cmain] if os.path.exists(cmain) else [])
+        key = _hash(deps + _headers() + [LIB], CFLAGS)
         stamp = exe + ".stamp"
         if not (os.path.exists(exe) and os.path.exists(stamp) and open(stamp).read() == key):
-            cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
-                   "-I" + os.path.join(ROOT, "include"), src, "-o", exe + ".tmp", "-L" + OUT,
-                   "-lhclib_amd", "-Wl,-rpath,$ORIGIN/.."]
-            r = subprocess.run(cmd, capture_output=True, text=True)
-            if r.returncode != 0:
-                raise RuntimeError(f"hipcc failed for {f}:\n{r.stderr[-6000:]}")
+            hip = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
+                   "-I" + os.path.join(ROOT, "include")]
+            link = ["-L" + OUT, "-lhclib_amd", "-Wl,-rpath,$ORIGIN/.."]
+            if os.path.exists(cmain):
+                steps = [hip + ["-c", src, "-o", exe + ".kinds.o"],
+                         ["gcc", "-std=gnu11", "-O2", "-Wall", "-I" + os.path.join(ROOT, "include"), "-c", cmain,
+                          "-o", exe + ".main.o"],
+                         [HIPCC, f"--offload-arch={ARCH}", exe + ".main.o", exe + ".kinds.o", "-o", exe + ".tmp"] + link]
+            else:
+                steps = [hip + [src, "-o", exe + ".tmp"] + link]
+            for cmd in steps:
+                r = subprocess.run(cmd, capture_output=True, text=True)
+                if r.returncode != 0:
+                    raise RuntimeError(f"build failed for {f}:\n{r.stderr[-6000:]}")
+            for tmp in (exe + ".kinds.o", exe + ".main.o"):
+                if os.path.exists(tmp):
+                    os.remove(tmp)
             os.replace(exe + ".tmp", exe)
             with open(stamp, "w") as fh:
                 fh.write(key)

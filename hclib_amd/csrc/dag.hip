@@ -164,7 +164,7 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
     HX_HIP(hipGetLastError());
     HX_HIP(hipEventRecord(m.ev1, m.stream));
     uint32_t err = 0;
-    unsigned long long st[3] = {0, 0, 0};
+    unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
     HX_HIP(hipMemcpyAsync(&err, v.err, 4, hipMemcpyDeviceToHost, m.stream));
     HX_HIP(hipMemcpyAsync(st, v.stats, sizeof(st), hipMemcpyDeviceToHost, m.stream));
     std::vector<uint32_t> sat;
@@ -178,6 +178,11 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
     for (size_t p = 0; p < sat.size(); ++p) satisfied_out[p] = sat[p] ? 1 : 0;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
+#if defined(HX_STAMPS) && HX_STAMPS
+    if (st[0] && (st[3] | st[4] | st[5]))
+        fprintf(stderr, "dag group phases (cycles per task, wave 0): take %.0f body %.0f put %.0f\n",
+                (double)st[3] / st[0], (double)st[4] / st[0], (double)st[5] / st[0]);
+#endif
     if (stats) {
         stats->tasks = st[0];
         stats->puts = st[1];

@@ -320,6 +320,66 @@ extern "C" int hclib_hip_forasync_triad_f32(float *a, const float *b, const floa
     return HCLIB_HIP_OK;
 }
 
+extern "C" int hclib_hip_forasync_plan(int dim, hclib_hip_loop_domain_t *domain, int mode, void *stream,
+                                       hclib_hip_sweep_plan_t *plan) {
+    static_assert(sizeof(hclib_hip_run_t) == sizeof(Run), "hclib_hip_run_t is hclib_sets::Run");
+    if (!domain || !plan || dim < 1 || dim > 3 || (mode != 0 && mode != 1)) {
+        set_error("hclib_hip_forasync_plan: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    memset(plan, 0, sizeof(*plan));
+    HX_TRY(ensure_device());
+    const int nworkers = hclib_hip_num_workers();
+    for (int d = 0; d < dim; ++d) {
+        if (domain[d].stride < 1) {
+            set_error("hclib_hip_forasync_plan: stride must be >= 1");
+            return HCLIB_HIP_EINVAL;
+        }
+        if (domain[d].tile == -1)  // src/hclib.c:455-461, written back
+            domain[d].tile = ((domain[d].high - domain[d].low) + nworkers - 1) / nworkers;
+        if (domain[d].tile < 1) domain[d].tile = 1;
+    }
+    std::vector<Run> runs[3];
+    std::vector<int64_t> pre[3];
+    size_t bytes = 0;
+    plan->ndim = dim;
+    plan->total = 1;
+    for (int d = 0; d < dim; ++d) {
+        runs[d] = dim_runs(domain[d], dim, mode);
+        pre[d].resize(runs[d].size() + 1);
+        pre[d][0] = 0;
+        for (size_t r = 0; r < runs[d].size(); ++r) pre[d][r + 1] = pre[d][r] + runs[d][r].count;
+        if (runs[d].empty()) runs[d].push_back(Run{0, 0, 1, 0});
+        bytes += ((runs[d].size() * sizeof(Run) + 15) & ~(size_t)15) + ((pre[d].size() * 8 + 15) & ~(size_t)15);
+        plan->total *= pre[d].back();
+    }
+    if (plan->total == 0) return HCLIB_HIP_OK;
+    hipStream_t st = (hipStream_t)stream;
+    char *dbuf = nullptr;
+    HX_HIP(hipMallocAsync((void **)&dbuf, bytes, st));
+    std::vector<char> hbuf(bytes);
+    size_t off = 0;
+    for (int d = 0; d < dim; ++d) {
+        memcpy(&hbuf[off], runs[d].data(), runs[d].size() * sizeof(Run));
+        plan->runs[d] = (const hclib_hip_run_t *)(dbuf + off);
+        off += (runs[d].size() * sizeof(Run) + 15) & ~(size_t)15;
+        memcpy(&hbuf[off], pre[d].data(), pre[d].size() * 8);
+        plan->prefix[d] = (const int64_t *)(dbuf + off);
+        off += (pre[d].size() * 8 + 15) & ~(size_t)15;
+        plan->nruns[d] = (int)runs[d].size();
+    }
+    HX_HIP(hipMemcpyAsync(dbuf, hbuf.data(), bytes, hipMemcpyHostToDevice, st));
+    plan->mem = dbuf;
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_forasync_plan_release(hclib_hip_sweep_plan_t *plan, void *stream) {
+    if (!plan) return HCLIB_HIP_EINVAL;
+    if (plan->mem) HX_HIP(hipFreeAsync(plan->mem, (hipStream_t)stream));
+    plan->mem = nullptr;
+    return HCLIB_HIP_OK;
+}
+
 extern "C" int hclib_hip_forasync(int body, const void *args, int dim,
                                   hclib_hip_loop_domain_t *domain, int mode, void *stream) {
     if (!args || !domain || dim < 1 || dim > 3 || (mode != 0 && mode != 1) ||

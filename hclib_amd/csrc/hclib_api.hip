@@ -52,8 +52,21 @@ struct Runtime {
     bool launched = false;
     bool hip = false;
     std::vector<hclib_task_t *> ready;  // LIFO, like the owner end of a deque
-    std::map<generic_frame_ptr, int> kinds;
-    std::map<void *, int> bodies;
+    // the kind table: device task kinds and device loop bodies by the host
+    // function that names them; built-in (fib, UTS, the library's loop
+    // bodies, by id) or a user launcher from the program's own HIP object
+    struct DevKind {
+        int builtin = 0;
+        hclib_hip_async_launcher_t launch = nullptr;
+        std::string name;
+    };
+    struct DevBody {
+        int builtin = 0;
+        hclib_hip_forasync_launcher_t launch = nullptr;
+        std::string name;
+    };
+    std::map<generic_frame_ptr, DevKind> kinds;
+    std::map<void *, DevBody> bodies;
     // memory callbacks per locale type (src/hclib-mem.c:13-50)
     struct MemFuncs {
         hclib_module_alloc_impl_func_type alloc = nullptr;
@@ -172,18 +185,24 @@ void add_sched_counters(Runtime &R) {
     }
 }
 
-int kind_of(generic_frame_ptr fp) {
+const Runtime::DevKind *kind_of(generic_frame_ptr fp) {
     Runtime &R = rt();
-    if (R.kinds.empty()) return 0;
+    if (R.kinds.empty()) return nullptr;
     auto k = R.kinds.find(fp);
-    return k == R.kinds.end() ? 0 : k->second;
+    return k == R.kinds.end() ? nullptr : &k->second;
 }
 
 // run one device task kind to completion and write its outputs back
-void run_device_task(hclib_task_t *t, int kind) {
+void run_device_task(hclib_task_t *t, const Runtime::DevKind &dk) {
     Runtime &R = rt();
     ensure_gpu("device task", device_of(t->locale));
     R.device_tasks++;
+    if (dk.launch) {  // a user kind: its launcher runs it on the bound GPU
+        check_hip(dk.launch(t->args), dk.name.c_str());
+        add_sched_counters(R);
+        return;
+    }
+    const int kind = dk.builtin;
     switch (kind) {
     case HCLIB_HIP_KIND_FIB: {
         // FibArgs of test/fib/fib.c:50-53: { int n; long res; }
@@ -244,8 +263,8 @@ void execute(hclib_task_t *t) {
     if (t == g_root_task) {
         R.host_tasks++;
         run_root(t);
-    } else if (const int kind = kind_of(t->_fp)) {
-        run_device_task(t, kind);
+    } else if (const Runtime::DevKind *dk = kind_of(t->_fp)) {
+        run_device_task(t, *dk);
     } else {
         R.host_tasks++;
         t->_fp(t->args);
@@ -670,7 +689,15 @@ void hclib_forasync(void *fct, void *argv, int dim, hclib_loop_domain_t *domain,
     hclib_hip_loop_domain_t *d = (hclib_hip_loop_domain_t *)domain;
     hipStream_t st = hx::mod().stream;
     int rc;
-    if (b->second == HCLIB_HIP_BODY_IOTA_CHECK) {
+    if (b->second.launch) {
+        // a user body: its launcher enqueues the sweep on the module stream;
+        // it completes with the enclosing finish, as the built-in bodies do
+        rc = b->second.launch(argv, dim, domain, (int)mode, st);
+        check_hip(rc, b->second.name.c_str());
+        add_device_op(st, nullptr, nullptr);
+        return;
+    }
+    if (b->second.builtin == HCLIB_HIP_BODY_IOTA_CHECK) {
         // test/c/forasync1DCh.c passes a plain host int array: the sweep runs
         // on a device copy, copied back when the sweep completes
         hclib_hip_loop_domain_t dd = d[0];
@@ -688,13 +715,13 @@ void hclib_forasync(void *fct, void *argv, int dim, hclib_loop_domain_t *domain,
             hipMemsetAsync(op->dev_err, 0, sizeof(int), st) != hipSuccess)
             die("hclib_forasync: upload failed");
         hclib_hip_iota_args_t ia = {op->dev_ran, op->dev_err};
-        rc = hclib_hip_forasync(b->second, &ia, dim, d, mode, st);
+        rc = hclib_hip_forasync(b->second.builtin, &ia, dim, d, mode, st);
         check_hip(rc, "hclib_hip_forasync");
         add_device_op(st, iota_done, op);
     } else {
         // the sweep belongs to the enclosing finish: it completes there (or
         // in whatever helps first), the host thread does not wait for it here
-        rc = hclib_hip_forasync(b->second, argv, dim, d, mode, st);
+        rc = hclib_hip_forasync(b->second.builtin, argv, dim, d, mode, st);
         check_hip(rc, "hclib_hip_forasync");
         add_device_op(st, nullptr, nullptr);
     }
@@ -1037,14 +1064,49 @@ hclib_locale_t *hclib_hip_gpu_locale(int index) {
 
 void hclib_hip_register_async_kind(generic_frame_ptr fp, int kind) {
     if (kind != HCLIB_HIP_KIND_FIB && kind != HCLIB_HIP_KIND_UTS)
-        die("hclib_hip_register_async_kind: unknown kind %d", kind);
-    rt().kinds[fp] = kind;
+        die("hclib_hip_register_async_kind: unknown kind %d (the built-in kinds are HCLIB_HIP_KIND_FIB and "
+            "HCLIB_HIP_KIND_UTS; a kind of the program's own registers a launcher with "
+            "hclib_hip_register_device_async)", kind);
+    Runtime::DevKind k;
+    k.builtin = kind;
+    k.name = kind == HCLIB_HIP_KIND_FIB ? "fib" : "uts";
+    rt().kinds[fp] = k;
 }
 
 void hclib_hip_register_forasync_body(void *fct, int body) {
     if (body < HCLIB_HIP_BODY_TRIAD_F32 || body > HCLIB_HIP_BODY_VISIT_COUNT)
-        die("hclib_hip_register_forasync_body: unknown body %d", body);
-    rt().bodies[fct] = body;
+        die("hclib_hip_register_forasync_body: unknown body %d (the built-in bodies are "
+            "HCLIB_HIP_BODY_TRIAD_F32..HCLIB_HIP_BODY_VISIT_COUNT; a body of the program's own registers a "
+            "launcher with hclib_hip_register_device_forasync)", body);
+    Runtime::DevBody b;
+    b.builtin = body;
+    b.name = "built-in body";
+    rt().bodies[fct] = b;
+}
+
+// the kind table entries of the program's own HIP objects
+// (HCLIB_HIP_DEVICE_ASYNC / HCLIB_HIP_DEVICE_FORASYNC, include/hclib_hip_cpp.h)
+void hclib_hip_register_device_async(generic_frame_ptr fp, const char *name, hclib_hip_async_launcher_t launch) {
+    if (!fp || !launch) die("hclib_hip_register_device_async: null function or launcher");
+    Runtime::DevKind k;
+    k.launch = launch;
+    k.name = name ? name : "device kind";
+    rt().kinds[fp] = k;
+}
+
+void hclib_hip_register_device_forasync(void *fct, const char *name, hclib_hip_forasync_launcher_t launch) {
+    if (!fct || !launch) die("hclib_hip_register_device_forasync: null body or launcher");
+    Runtime::DevBody b;
+    b.launch = launch;
+    b.name = name ? name : "device body";
+    rt().bodies[fct] = b;
+}
+
+int hclib_hip_device_kind_count(void) { return (int)rt().kinds.size(); }
+
+const char *hclib_hip_device_kind_name(generic_frame_ptr fp) {
+    const Runtime::DevKind *k = kind_of(fp);
+    return k ? k->name.c_str() : nullptr;
 }
 
 // hclib_print_runtime_stats, src/hclib-runtime.c:1370-1410: the reference's

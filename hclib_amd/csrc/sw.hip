@@ -57,7 +57,8 @@ struct SwCtx {
     int progressive;  // row schedule: chunked bottom-row hand-off
     const int *left_in;  // [nth*th]
     int *right_out;      // [nth*th]
-    int form;            // multi-wave bands: 10 * skew + hand-off steps / 16
+    int form;            // multi-wave bands: 100 * rows per lane + 10 * skew + hand-off steps / 16
+    int bh;              // multi-wave band height (64 * rows per lane)
 };
 
 // alignment_score_matrix (smith_waterman.cpp:36-43) row for s2 code a, plus
@@ -564,13 +565,25 @@ __host__ __device__ inline size_t sw_band_lds_bytes(int nw) {
            + 2 * 64 * 4;                          // prod / cons words
 }
 
-// the multi-wave kernel's shape: 64-row bands, 1..14 compute waves per tile
-// row (+ the ingress and egress waves)
-inline bool sw_band_ok(int th) { return th % 64 == 0 && th / 64 >= 1 && th / 64 <= 14; }
-// tile rows per workgroup: as many as 14 compute waves hold (fewer hand-offs
-// through global memory), HCLIB_HIP_SW_ROWS_PER_WG overrides
-inline int sw_band_rows_per_wg(int th) {
-    const int bpt = th / 64, most = 14 / bpt;
+// the multi-wave kernel's shape: bands of bh = 64 or 128 rows, 1..14 compute
+// waves per tile row (+ the ingress and egress waves)
+inline bool sw_band_ok(int th, int bh) { return th % bh == 0 && th / bh >= 1 && th / bh <= 14; }
+// HCLIB_HIP_SW_FORM (default `def`), kept to a valid form for th: two rows
+// per lane need th % 128 == 0, else one row per lane with the same hand-off
+inline int sw_pick_form(int th, int def) {
+    int form = env_int("HCLIB_HIP_SW_FORM", def);
+    if (form != 11 && form != 12 && form != 21 && form != 22 && form != 211 && form != 212 && form != 214 &&
+        form != 411 && form != 412 && form != 414)
+        form = def;
+    if (form > 400 && th % 256 != 0) form -= 200;
+    if (form > 200 && th % 128 != 0) form -= 200;
+    return form;
+}
+inline int sw_form_bh(int form) { return 64 * (form > 100 ? form / 100 : 1); }
+// tile rows per workgroup (HCLIB_HIP_SW_ROWS_PER_WG, default 1): more share
+// the CU's SIMDs between more waves and measured slower (scripts/probe_sw.py)
+inline int sw_band_rows_per_wg(int th, int bh) {
+    const int bpt = th / bh, most = 14 / bpt;
     int k = env_int("HCLIB_HIP_SW_ROWS_PER_WG", 1);
     return k < 1 ? 1 : (k > most ? most : k);
 }
@@ -650,6 +663,54 @@ __device__ __forceinline__ void sw_band_sub(int s, int ncols, const int *top4, c
     }
 }
 
+// The same K steps with R = 2 or 4 rows per lane (skew 1): lane L owns rows
+// R L .. R L + R - 1 of a 64 R-row band; the cell above the lane's first row
+// comes from lane L-1's last row, each other row's from the row before it in
+// the same column. One DPP shift and one ring write serve R cells, and a
+// 256-row tile needs 4 / R waves, so fewer hand-off lags are paid.
+template <bool MASK, int K, int R>
+__device__ __forceinline__ void sw_band_subR(int s, int ncols, const int *top4, const uint32_t *code4, int *wb,
+                                             const uint32_t (&mrow)[R], int (&lr)[R], int &diag) {
+    constexpr int G = K / 4;
+    const int lane = lane_id();
+    int4 tn = *(const int4 *)top4, tn2 = *(const int4 *)(top4 + 4);
+    uint32_t cn = code4[0], cn2 = code4[1];
+#pragma unroll
+    for (int m = 0; m < G; ++m) {
+        const int4 tc = tn;
+        const uint32_t cc = cn;
+        tn = tn2;
+        cn = cn2;
+        if (m + 2 < G) {
+            tn2 = *(const int4 *)(top4 + 4 * (m + 2));
+            cn2 = code4[m + 2];
+        }
+        uint32_t sc[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) sc[q] = __builtin_amdgcn_perm(0u, mrow[q], cc);
+        const int tv[4] = {tc.x, tc.y, tc.z, tc.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = 4 * m + j;
+            const int up0 = __builtin_amdgcn_update_dpp(tv[j], lr[R - 1], 0x138, 0xf, 0xf, false);
+            const bool v = !MASK || (unsigned)(s + k - lane) < (unsigned)ncols;
+            int up = up0, dg = diag;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const int d = dg + (int)(int8_t)(sc[q] >> (8 * j));
+                const int a = lr[q] > up ? lr[q] : up;
+                int h = a > d ? a : d;
+                if (MASK) h = v ? h : lr[q];
+                dg = lr[q];
+                lr[q] = h;
+                up = h;
+            }
+            diag = MASK ? (v ? up0 : diag) : up0;
+            wb[k] = lr[R - 1];
+        }
+    }
+}
+
 // Wait for an LDS flag. The device error word and the clock are looked at
 // only every 64 polls: a global load here would wait for all of the wave's
 // outstanding global memory operations.
@@ -679,7 +740,7 @@ __device__ bool sw_band_spin(const SwCtx &c, const int *flag, int want, unsigned
 // the promise DAG reads and writes the reference's plain arrays (its inputs
 // are complete before it runs).
 struct SwBand {
-    int R0, C0, ncols, nb;
+    int R0, C0, ncols, nb, bh;  // nb bands of bh = 64 R rows
     const int *leftcol;  // H(R0 + 1 + k, C0), k < 64 nb; null when C0 == 0
     int corner_h;        // H(R0, C0)
     int *rightcol;       // H(R0 + 1 + k, C0 + ncols) out, or null
@@ -688,6 +749,11 @@ struct SwBand {
     unsigned long long *gout;       // bottom row as tagged granules, or
     int *hout;                      // as plain H, with
     int *corner_out;                //   its last value here (may be null)
+    // DAG tile tasks: the left column / the next corner through LDS when the
+    // workgroup ran the left neighbour itself (null / false otherwise)
+    bool left_lds;       // leftcol points to LDS (plain loads)
+    int *rightcol_lds;   // also keep the right column here
+    int *corner_lds;     // H(R0, C0 + ncols): the right neighbour's corner
 };
 
 // The workgroup's ingress wave: moves the top row into ring 0 and publishes
@@ -724,10 +790,32 @@ __device__ bool sw_band_ingress(const SwCtx &c, const SwBand &B, int *ring0, int
             if (lane < m) ring0[x0 & (kSwRing - 1)] = (int)(uint32_t)a + ga;
             if (lane + 64 < m) ring0[x1 & (kSwRing - 1)] = (int)(uint32_t)b + gb;
         } else {
-            // complete inputs (a DAG tile's) or the boundary row, H(0, c) = -c
-            ring0[x0 & (kSwRing - 1)] = B.hin ? ld_agent(&B.hin[xa]) + ga : 0;
-            ring0[x1 & (kSwRing - 1)] = B.hin ? ld_agent(&B.hin[xb]) + gb : 0;
-            m = 128;
+            // complete inputs (a DAG tile's) or the boundary row, H(0, c) = -c:
+            // 256 columns per round trip (four loads per lane in flight)
+            const int x2 = x0 + 128, x3 = x0 + 192;
+            const int xc = x2 < ncols ? x2 : ncols - 1, xd = x3 < ncols ? x3 : ncols - 1;
+            int ha = 0, hb = 0, hc = 0, hd = 0;
+            if (B.hin) {
+                ha = ld_agent(&B.hin[xa]);
+                hb = ld_agent(&B.hin[xb]);
+                if (next + 128 < ncols) {
+                    hc = ld_agent(&B.hin[xc]);
+                    hd = ld_agent(&B.hin[xd]);
+                }
+            }
+            const bool four = next + 128 < ncols && next + 256 - kSwRing <= lds_flag_ld(&cons[0]);
+            if (B.corner_lds) {  // H(R0, C0 + ncols): the top row's last value
+                const int lx = ncols - 1 - next;
+                const int hl = !B.hin ? -(B.C0 + ncols) : (lx == lane ? ha : lx == lane + 64 ? hb : lx == lane + 128 ? hc : hd);
+                if (lx >= 0 && lx < 256 && (lx & 63) == lane) *B.corner_lds = hl;
+            }
+            ring0[x0 & (kSwRing - 1)] = B.hin ? ha + ga : 0;
+            ring0[x1 & (kSwRing - 1)] = B.hin ? hb + gb : 0;
+            if (four) {
+                ring0[x2 & (kSwRing - 1)] = B.hin ? hc + B.R0 + (B.C0 + x2 + 1) : 0;
+                ring0[x3 & (kSwRing - 1)] = B.hin ? hd + B.R0 + (B.C0 + x3 + 1) : 0;
+            }
+            m = four ? 256 : 128;
         }
         if (m > 0) {
             next = next + m < ncols ? next + m : ncols;
@@ -751,7 +839,7 @@ __device__ bool sw_band_ingress(const SwCtx &c, const SwBand &B, int *ring0, int
 // cons[nb]; the compute waves issue no global stores but the right column.
 __device__ bool sw_band_egress(const SwCtx &c, const SwBand &B, int *ring, int *prod, int *cons) {
     const int lane = lane_id();
-    const int ncols = B.ncols, nb = B.nb, Rb = B.R0 + 64 * nb;  // matrix row of the bottom row
+    const int ncols = B.ncols, nb = B.nb, Rb = B.R0 + B.bh * nb;  // matrix row of the bottom row
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     int next = 0;
     while (next < ncols) {
@@ -776,9 +864,10 @@ __device__ bool sw_band_egress(const SwCtx &c, const SwBand &B, int *ring, int *
 // skew S, hand-offs every K steps. Returns false on a device error.
 // Diagnostic build only (HX_STAMPS): ph[0] compute, [1] waiting for the top
 // row, [2] waiting for ring space + staging codes, [3] publishing (cycles).
-template <int S, int K>
+template <int S, int K, int R>
 __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, int *dummy, uint8_t *code_rings,
                             int *prod, int *cons, unsigned long long *ph, bool stamp_first) {
+    static_assert(R == 1 || S == 1, "several rows per lane only with skew 1");
     constexpr int D = 63 * S;        // lane 63's lag in steps
     constexpr int CR = S == 1 ? 128 : 256;  // code ring columns (needs D + 64)
     unsigned long long ts = sw_stamp();
@@ -793,15 +882,25 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
     const int C0 = B.C0, ncols = B.ncols;
     int *ring_in = rings + (size_t)w * kSwRingStride, *ring_out = ring_in + kSwRingStride;
     uint8_t *cr = code_rings + w * 2048;
-    const int r = B.R0 + w * 64 + lane + 1;  // this lane's matrix row
+    const int r = B.R0 + w * 64 * R + R * lane + 1;  // this lane's (first) matrix row
     const uint32_t mrow = sw_row2(c.s2[r - 1]);
     // G at (r, C0) and (r - 1, C0): the band's left column
     auto left_h = [&](int row) {
-        return C0 == 0 ? -row : (row == B.R0 ? B.corner_h : ld_agent(&B.leftcol[row - B.R0 - 1]));
+        return C0 == 0 ? -row
+                       : (row == B.R0 ? B.corner_h
+                                      : (B.left_lds ? B.leftcol[row - B.R0 - 1] : ld_agent(&B.leftcol[row - B.R0 - 1])));
     };
     int left = left_h(r) + r + C0;
     int diag = left_h(r - 1) + (r - 1) + C0;
     int o2 = left;
+    // R > 1: the lane's rows r .. r + R - 1 (lr[0] is `left`'s role)
+    uint32_t mr[R];
+    int lr[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        mr[q] = sw_row2(c.s2[r - 1 + q]);
+        lr[q] = left_h(r + q) + (r + q) + C0;
+    }
     int *wbase = lane == 63 ? ring_out : dummy + w * 128 + lane;
     const int8_t *s1 = c.s1 + C0;
     // s1 code (1..4) of column x; loads clamped to the band, never predicated,
@@ -833,7 +932,7 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
         const uint32_t *cb = (const uint32_t *)(cr + cofs * 2 * CR + ((s0 - S * lane + cofs) & (CR - 1)));
         int *wb = wbase + (lane == 63 ? ((s0 - D) & (kSwRing - 1)) : 0);
         const bool full = s0 >= D && s0 + 64 <= ncols;
-        phase(2);
+        phase(s0 == 0 ? 4 : 2);
 #pragma unroll
         for (int q = 0; q < 64 / K; ++q) {
             const int s = s0 + q * K;
@@ -845,21 +944,29 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
             if (HX_STAMPS && s == 0 && w == 0 && lane == 0 && stamp_first) {
                 // first input of the tile row (global clock): rows' start spacing
                 const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-                if (B.R0 == c.i0 * c.th) st_agent(&c.stats[21], now);
-                if (B.R0 + 64 * B.nb == c.i1 * c.th) st_agent(&c.stats[20], now);
+                if (B.R0 == c.i0 * c.th) st_agent(&c.stats[27], now);
+                if (B.R0 + B.bh * B.nb == c.i1 * c.th) st_agent(&c.stats[26], now);
             }
             phase(1);
-            if (full)
+            if (R > 1) {
+                if (full)
+                    sw_band_subR<false, K, R>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mr, lr,
+                                              diag);
+                else
+                    sw_band_subR<true, K, R>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mr, lr,
+                                             diag);
+            } else if (full) {
                 sw_band_sub<false, S, K>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mrow, left,
                                          diag, o2);
-            else
+            } else {
                 sw_band_sub<true, S, K>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mrow, left,
                                         diag, o2);
+            }
             phase(0);
             // lane 63's last S columns of the chunk may have gone past the
             // ring's end (wrap slots): they are also stored at their own slots
             if (q == 64 / K - 1 && lane == 63) {
-                ring_out[(s0 + 63 - D) & (kSwRing - 1)] = left;
+                ring_out[(s0 + 63 - D) & (kSwRing - 1)] = R > 1 ? lr[R - 1] : left;
                 if (S == 2) ring_out[(s0 + 62 - D) & (kSwRing - 1)] = o2;
             }
             // publish: ring_out holds columns < s + K - D, ring_in's columns
@@ -873,21 +980,37 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
         }
         stage_codes(s0 + 64 + lane, craw);
     }
-    if (HX_STAMPS && stamp_first && w == B.nb - 1 && lane == 0 && B.R0 + 64 * B.nb == c.i1 * c.th)
-        st_agent(&c.stats[22], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    if (ok && B.rightcol) st_agent(&B.rightcol[r - B.R0 - 1], left - r - (C0 + ncols));
+    if (HX_STAMPS && stamp_first && w == B.nb - 1 && lane == 0 && B.R0 + B.bh * B.nb == c.i1 * c.th)
+        st_agent(&c.stats[28], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (ok && B.rightcol) {
+        if (R == 1) st_agent(&B.rightcol[r - B.R0 - 1], left - r - (C0 + ncols));
+#pragma unroll
+        for (int q = 0; R > 1 && q < R; ++q) st_agent(&B.rightcol[r - B.R0 - 1 + q], lr[q] - (r + q) - (C0 + ncols));
+    }
+    if (ok && B.rightcol_lds) {
+        if (R == 1) B.rightcol_lds[r - B.R0 - 1] = left - r - (C0 + ncols);
+#pragma unroll
+        for (int q = 0; R > 1 && q < R; ++q) B.rightcol_lds[r - B.R0 - 1 + q] = lr[q] - (r + q) - (C0 + ncols);
+    }
     return ok;
 }
 
-// the (skew, hand-off) forms: HCLIB_HIP_SW_FORM = 10 S + K / 16
+// the (rows per lane, skew, hand-off) forms: HCLIB_HIP_SW_FORM =
+// 100 R + 10 S + K / 16 (sw_pick_form keeps to the valid ones)
 __device__ __forceinline__ bool sw_band_row_any(int form, const SwCtx &c, const SwBand &B, int w, int *rings,
                                                 int *dummy, uint8_t *code_rings, int *prod, int *cons,
                                                 unsigned long long *ph, bool stamp_first) {
     switch (form) {
-        case 11: return sw_band_row<1, 16>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
-        case 12: return sw_band_row<1, 32>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
-        case 21: return sw_band_row<2, 16>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
-        default: return sw_band_row<2, 32>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 11: return sw_band_row<1, 16, 1>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 12: return sw_band_row<1, 32, 1>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 21: return sw_band_row<2, 16, 1>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 22: return sw_band_row<2, 32, 1>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 211: return sw_band_row<1, 16, 2>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 212: return sw_band_row<1, 32, 2>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 411: return sw_band_row<1, 16, 4>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 412: return sw_band_row<1, 32, 4>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 214: return sw_band_row<1, 64, 2>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        default: return sw_band_row<1, 64, 4>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
     }
 }
 
@@ -897,7 +1020,7 @@ __device__ __forceinline__ bool sw_band_row_any(int form, const SwCtx &c, const 
 __global__ __launch_bounds__(1024) void k_sw_band_rows(SwCtx c) {
     extern __shared__ __attribute__((aligned(16))) int sw_lds[];
     const int nwave = (int)(blockDim.x >> 6) - 2, w = (int)(threadIdx.x >> 6);
-    const int bpt = c.th / 64, k = nwave / bpt;
+    const int bpt = c.th / c.bh, k = nwave / bpt;
     int *rings = sw_lds;
     int *dummy = rings + (size_t)(nwave + 1) * kSwRingStride;
     uint8_t *code_rings = (uint8_t *)(dummy + nwave * 128);
@@ -905,7 +1028,7 @@ __global__ __launch_bounds__(1024) void k_sw_band_rows(SwCtx c) {
     const size_t gstride = (size_t)c.ntw * c.tw;  // granules per tile row
     bool ok = true;
     unsigned long long ntile = 0;
-    unsigned long long ph[4] = {0, 0, 0, 0};
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
     // blocks of k tile rows; with the grid a multiple of the 8 XCDs, block
     // positions are dealt so that consecutive blocks run on one XCD (the
     // dispatcher places workgroup b on XCD b mod 8 — for speed only: every
@@ -920,6 +1043,7 @@ __global__ __launch_bounds__(1024) void k_sw_band_rows(SwCtx c) {
         B.C0 = c.j0 * c.tw;
         B.ncols = (c.j1 - c.j0) * c.tw;
         B.nb = kk * bpt;
+        B.bh = c.bh;
         B.leftcol = c.j0 > 0 ? c.left_in + B.R0 : nullptr;
         B.corner_h = B.R0 == 0 ? -B.C0 : (c.j0 == 0 ? -B.R0 : (c.j0 > 0 ? ld_agent(&c.left_in[B.R0 - 1]) : 0));
         B.rightcol = c.right_out ? c.right_out + B.R0 : nullptr;
@@ -928,6 +1052,9 @@ __global__ __launch_bounds__(1024) void k_sw_band_rows(SwCtx c) {
         B.gout = c.gbot + (size_t)(i + kk - 1) * gstride + B.C0;
         B.hout = nullptr;
         B.corner_out = nullptr;
+        B.left_lds = false;
+        B.rightcol_lds = nullptr;
+        B.corner_lds = nullptr;
         if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod[0..63], cons[0..63]
         __syncthreads();
         if (w == nwave)
@@ -942,7 +1069,7 @@ __global__ __launch_bounds__(1024) void k_sw_band_rows(SwCtx c) {
     }
     if (threadIdx.x == 0) add_agent(&c.stats[0], ntile);
     if (HX_STAMPS && lane_id() == 0 && w < 4)  // per compute wave (first four)
-        for (int q = 0; q < 4; ++q) add_agent(&c.stats[4 + 4 * w + q], ph[q]);
+        for (int q = 0; q < 6 && w < 3; ++q) add_agent(&c.stats[4 + 6 * w + q], ph[q]);
 }
 
 // The generic device promise DAG (include/hclib_hip/hx_dag.h) driving the
@@ -980,44 +1107,66 @@ __global__ __launch_bounds__(64) void k_sw_dag(SwCtx c, DagView v) {
 // promises are put by wave 0 once every wave's stores are drained.
 struct SwDagWgKind {
     using Ctx = SwCtx;
+    // every tile input from another task (top row, left column, corner) is
+    // read with ld_agent and written with st_agent: no fences needed
+    static constexpr bool kSc1Payload = true;
     __device__ static bool run_group(const SwCtx &c, uint32_t t, const uint32_t *, int wave) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
-        const int nw = c.th / 64;
+        const int nw = c.th / c.bh;
         int *rings = sw_lds;
         int *dummy = rings + (size_t)(nw + 1) * kSwRingStride;
         uint8_t *code_rings = (uint8_t *)(dummy + nw * 128);
         int *prod = (int *)(code_rings + nw * 2048), *cons = prod + 64;
+        // the workgroup's last tile: its right column (two buffers by tile
+        // parity) and its right neighbour's corner, for a row successor
+        int *last = cons + 64, *corner_keep = last + 1, *right_keep = last + 4;  // [2][th]
         const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
+        const bool from_lds = j > 0 && *last == (int)t - 1;
         SwBand B;
         B.R0 = i * c.th;
         B.C0 = j * c.tw;
         B.ncols = c.tw;
         B.nb = nw;
-        B.leftcol = j > 0 ? c.right + (size_t)(t - 1) * c.th : nullptr;
-        B.corner_h = B.R0 == 0 ? -B.C0 : (j == 0 ? -B.R0 : ld_agent(&c.corner[t - (uint32_t)c.ntw - 1]));
+        B.bh = c.bh;
+        B.left_lds = from_lds;
+        B.leftcol = j == 0 ? nullptr : (from_lds ? right_keep + ((t - 1) & 1) * c.th : c.right + (size_t)(t - 1) * c.th);
+        B.corner_h = B.R0 == 0 ? -B.C0
+                               : (j == 0 ? -B.R0 : (from_lds ? corner_keep[(t - 1) & 1]
+                                                             : ld_agent(&c.corner[t - (uint32_t)c.ntw - 1])));
+        B.rightcol_lds = right_keep + (t & 1) * c.th;
+        B.corner_lds = corner_keep + (t & 1);
         B.rightcol = c.right + (size_t)t * c.th;
         B.gin = nullptr;
         B.hin = i > 0 ? c.bottom + (size_t)(t - (uint32_t)c.ntw) * c.tw : nullptr;
         B.gout = nullptr;
         B.hout = c.bottom + (size_t)t * c.tw;
         B.corner_out = c.corner + t;
+        __syncthreads();  // every wave has read `last`
         if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod[0..63], cons[0..63]
+        if (threadIdx.x == 0) *last = (int)t;
         __syncthreads();
-        unsigned long long ph[4] = {0, 0, 0, 0};
+        unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
         if (wave == nw) return sw_band_ingress(c, B, rings, prod, cons);
         if (wave == nw + 1) return sw_band_egress(c, B, rings + (size_t)nw * kSwRingStride, prod, cons);
-        return sw_band_row_any(c.form, c, B, wave, rings, dummy, code_rings, prod, cons, ph, false);
+        const bool ok = sw_band_row_any(c.form, c, B, wave, rings, dummy, code_rings, prod, cons, ph, false);
+        if (HX_STAMPS && lane_id() == 0 && wave < 4)
+            for (int q = 0; q < 6 && wave < 3; ++q) add_agent(&c.stats[4 + 6 * wave + q], ph[q]);
+        return ok;
     }
     // right column, bottom row, corner (:212-226): one release for all three
     __device__ static void put(const SwCtx &c, DagWave &w, uint32_t t) {
         const uint32_t ps[3] = {3u * t + 0u, 3u * t + 1u, 3u * t + 2u};
         const unsigned long long ds[3] = {0ull, 0ull, (unsigned long long)(uint32_t)ld_agent(&c.corner[t])};
-        dag_put_n<3>(w, ps, ds);
+        dag_put_n<3, true>(w, ps, ds);
     }
 };
 
 __global__ __launch_bounds__(1024) void k_sw_dag_wg(SwCtx c, DagView v) {
+    extern __shared__ __attribute__((aligned(16))) int sw_lds[];
     __shared__ uint32_t task_slot;
+    const int nw = c.th / c.bh;
+    int *last = (int *)((uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * 128) + nw * 2048) + 128;
+    if (threadIdx.x == 0) *last = -2;  // no tile yet (run_dag_group's barriers order this)
     run_dag_group<SwDagWgKind>(c, v, &task_slot);
 }
 
@@ -1061,7 +1210,11 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     const bool rows = !(sched && (!strcmp(sched, "queue") || dag)) && rows_lds <= 64 * 1024;
     // multi-wave tile rows (th / 64 waves per workgroup) unless "rows1" asks
     // for the one-wave-per-tile-row kernel
-    const bool band_shape = sw_band_ok(th) && tw <= 65536;
+    // multi-wave band form (sw_pick_form): the DAG's tile tasks default to two
+    // rows per lane (two waves per 256-row tile: one hand-off lag instead of
+    // three), the row schedule to one
+    const int form = sw_pick_form(th, dag ? 212 : 12), bh = sw_form_bh(form);
+    const bool band_shape = sw_band_ok(th, bh) && tw <= 65536;
     const bool band = rows && band_shape && !(sched && !strcmp(sched, "rows1"));
     const size_t nt = ntw * nth;
     const size_t b_s1 = ntw * tw, b_s2 = nth * th;
@@ -1102,7 +1255,8 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     c.left_in = nullptr;
     c.right_out = nullptr;
     c.progressive = env_int("HCLIB_HIP_SW_PROGRESSIVE", 1);
-    c.form = env_int("HCLIB_HIP_SW_FORM", 12);
+    c.form = form;
+    c.bh = bh;
     int rc = HCLIB_HIP_OK;
     auto fail = [&](int r) { (void)hipFree(d); return r; };
     if ((rc = hip_check(hipMemcpyAsync((void *)c.s1, s1, b_s1, hipMemcpyHostToDevice, m.stream), "copy s1"))) return fail(rc);
@@ -1118,7 +1272,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     } else {
         hipLaunchKernelGGL(k_sw_init, dim3(1024), dim3(256), 0, m.stream, c.deps, c.ready, c.ntw, c.nth);
     }
-    const size_t lds = band ? sw_band_lds_bytes(th / 64)
+    const size_t lds = band ? sw_band_lds_bytes(th / bh)
                             : 2 * (size_t)(((tw + 1 + 3) & ~3) * 4) + 68 * 4 + 2 * (size_t)((tw + 3) & ~3) + 16 +
                                   (rows ? 2 * (size_t)(((th + 3) & ~3) * 4) : 0);
     if (lds > 160 * 1024) return fail((set_error("hclib_hip_sw: tile too large for LDS"), HCLIB_HIP_EINVAL));
@@ -1155,10 +1309,11 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
                                       nullptr, wg ? 1 : wpc, c.spin_ms, &L)))
             return fail(rc);
         if (wg) {
-            const size_t blds = sw_band_lds_bytes(th / 64);
+            const size_t blds = sw_band_lds_bytes(th / bh) + (4 + 2 * (size_t)th) * 4;  // + kept right columns
             if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_wg,
                                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
-            hipLaunchKernelGGL(k_sw_dag_wg, dim3(L.grid), dim3(th + 128), blds, m.stream, c, *(const DagView *)L.view);
+            hipLaunchKernelGGL(k_sw_dag_wg, dim3(L.grid), dim3(64 * (th / bh) + 128), blds, m.stream, c,
+                               *(const DagView *)L.view);
         } else {
             hipLaunchKernelGGL(k_sw_dag, dim3(L.grid), dim3(64), lds, m.stream, c, *(const DagView *)L.view);
         }
@@ -1166,12 +1321,12 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     } else {
         if ((rc = hip_check(hipEventRecord(m.ev0, m.stream), "event"))) return fail(rc);
         if (band) {
-            const int k = sw_band_rows_per_wg(th), nblk = ((int)nth + k - 1) / k;
+            const int k = sw_band_rows_per_wg(th, bh), nblk = ((int)nth + k - 1) / k;
             const int g = nblk < m.num_cus ? nblk : m.num_cus;
-            const size_t blds = sw_band_lds_bytes(k * (th / 64));
+            const size_t blds = sw_band_lds_bytes(k * (th / bh));
             if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_band_rows,
                                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
-            hipLaunchKernelGGL(k_sw_band_rows, dim3(g), dim3(k * th + 128), blds, m.stream, c);
+            hipLaunchKernelGGL(k_sw_band_rows, dim3(g), dim3(64 * k * (th / bh) + 128), blds, m.stream, c);
         } else if (rows && c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), lds, m.stream, c);
         else if (rows) hipLaunchKernelGGL(k_sw_rows<false>, dim3(grid), dim3(64), lds, m.stream, c);
         else hipLaunchKernelGGL(k_sw, dim3(grid), dim3(64), lds, m.stream, c);
@@ -1184,15 +1339,18 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     if ((rc = hip_check(hipStreamSynchronize(m.stream), "k_sw"))) return fail(rc);
     (void)hipMemcpy(&herr, c.err, 4, hipMemcpyDeviceToHost);
     (void)hipMemcpy(st, c.stats, sizeof(st), hipMemcpyDeviceToHost);
-    if (HX_STAMPS && band) {
-        unsigned long long t[23] = {0};
+    if (HX_STAMPS && (band || (dag && band_shape))) {
+        unsigned long long t[29] = {0};
         (void)hipMemcpy(t, c.stats, sizeof(t), hipMemcpyDeviceToHost);
-        for (int w = 0; w < 4 && w < th / 64; ++w)
-            fprintf(stderr, "sw band wave %d phases (cycles per row): compute %.0f wait-top %.0f wait-ring %.0f staging %.0f\n",
-                    w, (double)t[4 + 4 * w] / nth, (double)t[5 + 4 * w] / nth, (double)t[6 + 4 * w] / nth,
-                    (double)t[7 + 4 * w] / nth);
-        fprintf(stderr, "sw band: row start spacing %.3f us, last row %.3f us\n",
-                nth > 1 ? (double)(t[20] - t[21]) * 0.01 / (double)(nth - 1) : 0.0, (double)(t[22] - t[20]) * 0.01);
+        const double per = dag ? (double)nt : (double)nth;  // per tile (DAG) or per tile row
+        for (int w = 0; w < 3 && w < th / bh; ++w)
+            fprintf(stderr, "sw band wave %d phases (cycles per %s): compute %.0f wait-top %.0f chunk-top %.0f"
+                            " publish %.0f prologue %.0f\n",
+                    w, dag ? "tile" : "row", (double)t[4 + 6 * w] / per, (double)t[5 + 6 * w] / per,
+                    (double)t[6 + 6 * w] / per, (double)t[7 + 6 * w] / per, (double)t[8 + 6 * w] / per);
+        if (!dag)
+            fprintf(stderr, "sw band: row start spacing %.3f us, last row %.3f us\n",
+                    nth > 1 ? (double)(t[26] - t[27]) * 0.01 / (double)(nth - 1) : 0.0, (double)(t[28] - t[26]) * 0.01);
     } else if (HX_STAMPS && st[0])
         fprintf(stderr, "sw phases (cycles/tile): inputs %.0f band-setup %.0f ramp-in %.0f steady %.0f ramp-out %.0f outputs %.0f\n",
                 (double)st[4] / st[0], (double)st[5] / st[0], (double)st[6] / st[0], (double)st[7] / st[0],
@@ -1296,7 +1454,8 @@ extern "C" int hclib_hip_sw_band_begin(const int8_t *s1, size_t n1, const int8_t
     c.j0 = j0;
     c.j1 = j1;
     c.progressive = env_int("HCLIB_HIP_SW_PROGRESSIVE", 1);
-    c.form = env_int("HCLIB_HIP_SW_FORM", 12);
+    c.form = sw_pick_form(th, 12);
+    c.bh = sw_form_bh(c.form);
     c.spin_ms = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     h->lds = lds;
     h->grid_cap = m.num_cus;
@@ -1330,13 +1489,14 @@ extern "C" int hclib_hip_sw_band_rows(hclib_hip_sw_band_t *h, int i0, int i1, co
     int grid = i1 - i0;
     if (grid > h->grid_cap) grid = h->grid_cap;
     const char *sched = getenv("HCLIB_HIP_SW_SCHED");
-    if (sw_band_ok(c.th) && !(sched && !strcmp(sched, "rows1"))) {
-        const int k = sw_band_rows_per_wg(c.th), nblk = (i1 - i0 + k - 1) / k;
+    if (sw_band_ok(c.th, c.bh) && !(sched && !strcmp(sched, "rows1"))) {
+        const int k = sw_band_rows_per_wg(c.th, c.bh), nblk = (i1 - i0 + k - 1) / k;
         const int g = nblk < h->grid_cap ? nblk : h->grid_cap;
-        const size_t blds = sw_band_lds_bytes(k * (c.th / 64));
+        const size_t blds = sw_band_lds_bytes(k * (c.th / c.bh));
         if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_band_rows,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
-        hipLaunchKernelGGL(k_sw_band_rows, dim3(g), dim3(k * c.th + 128), blds, (hipStream_t)stream, c);
+        hipLaunchKernelGGL(k_sw_band_rows, dim3(g), dim3(64 * k * (c.th / c.bh) + 128), blds, (hipStream_t)stream,
+                           c);
     }
     else if (c.progressive) hipLaunchKernelGGL(k_sw_rows<true>, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);
     else hipLaunchKernelGGL(k_sw_rows<false>, dim3(grid), dim3(64), h->lds, (hipStream_t)stream, c);

@@ -161,6 +161,27 @@ hclib_locale_t *hclib_hip_gpu_locale(int index);
 void hclib_hip_register_async_kind(generic_frame_ptr fp, int kind);
 void hclib_hip_register_forasync_body(void *forasync_fct, int body);
 
+/* The kind table of the program's own device code: a HIP translation unit
+ * the program links names, for a host function of the program, the launcher
+ * that runs it on the bound GPU (HCLIB_HIP_DEVICE_ASYNC /
+ * HCLIB_HIP_DEVICE_FORASYNC in include/hclib_hip_cpp.h register them before
+ * main). An async of a registered function runs its launcher instead of the
+ * host function; a forasync of a registered body enqueues the launcher's
+ * sweep, which completes with the enclosing finish. Launchers return
+ * HCLIB_HIP_OK or a negative HCLIB_HIP_E* code (include/hclib_hip.h); a
+ * failing launcher ends the program with its message, as a failing device
+ * kind does. Kinds and bodies outside the table are refused (the register
+ * calls above only take the built-in ids). */
+typedef int (*hclib_hip_async_launcher_t)(void *args);
+typedef int (*hclib_hip_forasync_launcher_t)(void *args, int dim, hclib_loop_domain_t *domain, int mode,
+                                             void *stream);
+void hclib_hip_register_device_async(generic_frame_ptr fp, const char *name, hclib_hip_async_launcher_t launch);
+void hclib_hip_register_device_forasync(void *forasync_fct, const char *name,
+                                        hclib_hip_forasync_launcher_t launch);
+/* registered device task kinds, and the name of one (NULL: not a kind) */
+int hclib_hip_device_kind_count(void);
+const char *hclib_hip_device_kind_name(generic_frame_ptr fp);
+
 typedef struct {
     int type, shape_fn, gen_mx, root_id, non_leaf_bf, compute_gran;
     double b_0, non_leaf_prob, shift_depth;

@@ -188,6 +188,29 @@ int hclib_hip_forasync_triad_f32(float *a, const float *b, const float *c, float
 /* Resident worker waves the forasync/megakernel launches use. */
 int hclib_hip_num_workers(void);
 
+/* The iteration set of hclib_hip_forasync, for device loop bodies compiled
+ * in the caller's own HIP translation unit (hclib::hip::forasync_device in
+ * include/hclib_hip_cpp.h): plan() applies the reference's tiling (tile ==
+ * -1 written back as in hclib_hip_forasync; FLAT and RECURSIVE sets exactly
+ * as src/hclib.c:110-464 enumerate them) and uploads one table of runs per
+ * dimension in `stream` order; iteration t of the sweep (0 <= t < total,
+ * innermost dimension fastest) maps to (i, j, k) through the runs. release()
+ * frees the tables in stream order after the sweep. */
+typedef struct {
+    int first, count, stride, pad;  /* indices first + m * stride, m < count */
+} hclib_hip_run_t;
+typedef struct {
+    const hclib_hip_run_t *runs[3];
+    const int64_t *prefix[3];  /* prefix[d][r] = iterations of dimension d before run r */
+    int nruns[3];
+    int ndim;
+    int64_t total;
+    void *mem;
+} hclib_hip_sweep_plan_t;
+int hclib_hip_forasync_plan(int dim, hclib_hip_loop_domain_t *domain, int mode, void *stream,
+                            hclib_hip_sweep_plan_t *plan);
+int hclib_hip_forasync_plan_release(hclib_hip_sweep_plan_t *plan, void *stream);
+
 /* ----------------------------------------------------------------- UTS */
 /* Tree parameters: the UTS CLI flags of test/uts/uts.c:380-420 (same field
  * order as oracle/uts_oracle.h so both sides read the same struct). */

@@ -142,10 +142,15 @@ __device__ __forceinline__ void dag_put(DagWave &w, uint32_t p, unsigned long lo
 // all N promises together (each lane one waiter of the concatenated lists),
 // then the released tasks take ready-list slots (one kept, as dag_put_one).
 // Waiter lists longer than 64 in total fall back to one put at a time.
-template <int N>
+// SC1 = true: the task wrote everything its waiters read with agent-scope
+// (sc1, write-through) stores, so draining them (vmcnt) is the release and
+// the L2 write-back of a release fence is skipped (MI355X_MICROARCH.md, Valid
+// forms: sc1 payload + drained counter, consumers read with sc1 loads).
+template <int N, bool SC1 = false>
 __device__ __forceinline__ void dag_put_n(DagWave &w, const uint32_t (&p)[N], const unsigned long long (&datum)[N]) {
     static_assert(N >= 1 && N <= 64, "dag_put_n: 1..64 promises");
-    release_agent();
+    if (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else release_agent();
     const DagView &v = w.v;
     const int lane = lane_id();
     uint32_t my_p = 0, b = 0, e = 0, was = 0;
@@ -295,12 +300,27 @@ __device__ void run_dag_worker(const typename Kind::Ctx &ctx, const DagView &vie
 // takes the tickets, as run_dag_worker does, and after the body — every
 // wave's stores drained, then a barrier — runs Kind::put(ctx, DagWave&, t),
 // the task's puts. `slot` is one LDS word for the task id broadcast.
-// Concept additions: run_group and put as above.
+// Concept additions: run_group and put as above, and kSc1Payload: true when
+// the bodies read what other tasks wrote only with agent-scope (sc1) loads,
+// so no acquire fence (an L2 invalidate) is needed before a body.
 template <class Kind>
 __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view, uint32_t *slot) {
     DagWave w{view, 0, 0, kDagEmpty, 0, 0};
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
     unsigned long long ran = 0;
+    // diagnostic build (HX_STAMPS): wave 0's cycles taking tasks / running
+    // bodies / putting, into stats[3..5]
+    unsigned long long cyc[3] = {0, 0, 0}, tsx = 0;
+    auto stamp = [&](int k) {
+#if defined(HX_STAMPS) && HX_STAMPS
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        if (tsx) cyc[k] += now - tsx;
+        tsx = now;
+#else
+        (void)k;
+#endif
+    };
+    stamp(0);
     while (true) {
         bool kept = false;
         uint32_t pend_pos = 0;
@@ -345,20 +365,26 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
         const uint32_t t = *slot;
         __syncthreads();  // the slot is rewritten only after this barrier
         if (t == kDagEmpty) break;
-        acquire_agent();
+        if (!Kind::kSc1Payload) acquire_agent();
+        stamp(0);
         const bool ok = Kind::run_group(ctx, t, view.payload + (size_t)t * view.payload_words, wave);
         vm_drain();
         if (__syncthreads_or(!ok)) break;
+        stamp(1);
         if (wave == 0) {
             Kind::put(ctx, w, t);
             if (kept && lane == pend_lane) st_agent(&view.ready[pend_pos], kDagSkip);
         }
+        stamp(2);
         ++ran;
     }
     if (wave == 0 && lane == 0) {
         add_agent(&view.stats[0], ran);
         add_agent(&view.stats[1], w.puts);
         add_agent(&view.stats[2], w.releases);
+#if defined(HX_STAMPS) && HX_STAMPS
+        for (int k = 0; k < 3; ++k) add_agent(&view.stats[3 + k], cyc[k]);
+#endif
     }
 }
 

@@ -56,6 +56,70 @@
 namespace hclib {
 namespace hip {
 
+// ------------------------------------------- device loop bodies of the caller
+// forasync_device(body, dim, domain, mode, stream): the reference's forasync
+// iteration set (hclib_hip_forasync_plan) swept by a kernel compiled here,
+// in the caller's translation unit; body(i, j, k) is a __device__ callable
+// (j, k = 0 below dim 2, 3). Asynchronous on `stream`.
+namespace detail {
+__device__ __forceinline__ int sweep_index(const hclib_hip_sweep_plan_t &p, int d, int64_t t) {
+    int lo = 0, hi = p.nruns[d] - 1;
+    while (lo < hi) {  // the last run with prefix <= t
+        const int mid = (lo + hi + 1) >> 1;
+        if (p.prefix[d][mid] <= t) lo = mid;
+        else hi = mid - 1;
+    }
+    const hclib_hip_run_t r = p.runs[d][lo];
+    return r.first + (int)(t - p.prefix[d][lo]) * r.stride;
+}
+template <class Body>
+__global__ __launch_bounds__(256) void k_user_sweep(Body body, hclib_hip_sweep_plan_t p) {
+    const int64_t n1 = p.ndim > 1 ? p.prefix[1][p.nruns[1]] : 1, n2 = p.ndim > 2 ? p.prefix[2][p.nruns[2]] : 1;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < p.total; t += step) {
+        const int64_t t2 = t % n2, r = t / n2, t1 = r % n1, t0 = r / n1;
+        body(sweep_index(p, 0, t0), p.ndim > 1 ? sweep_index(p, 1, t1) : 0, p.ndim > 2 ? sweep_index(p, 2, t2) : 0);
+    }
+}
+}  // namespace detail
+
+template <class Body>
+int forasync_device(const Body &body, int dim, hclib_loop_domain_t *domain, int mode, void *stream) {
+    static_assert(sizeof(hclib_loop_domain_t) == sizeof(hclib_hip_loop_domain_t), "hclib_loop_domain_t layout");
+    hclib_hip_sweep_plan_t p;
+    int rc = hclib_hip_forasync_plan(dim, (hclib_hip_loop_domain_t *)domain, mode, stream, &p);
+    if (rc || p.total == 0) return rc;
+    int64_t grid = (p.total + 255) / 256;
+    const int64_t cap = (int64_t)(hclib_hip_num_cus() > 0 ? hclib_hip_num_cus() : 1) * 16;
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(detail::k_user_sweep<Body>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, body, p);
+    if (hipGetLastError() != hipSuccess) rc = HCLIB_HIP_EHIP;
+    const int rr = hclib_hip_forasync_plan_release(&p, stream);
+    return rc ? rc : rr;
+}
+
+}  // namespace hip
+}  // namespace hclib
+
+// The kind table (include/hclib.h): register, before main, a launcher for a
+// host function of the program. `fp` is the function the program passes to
+// hclib_async / spawn (a device task kind) or to hclib_forasync (a device
+// loop body); `launcher` is int (void *args) resp. int (void *args, int dim,
+// hclib_loop_domain_t *domain, int mode, void *stream), defined in this
+// translation unit (typically run_tasks<Kind> / run_dag<Kind> /
+// forasync_device around the program's own device code).
+#define HCLIB_HIP_KIND_CAT2(a, b) a##b
+#define HCLIB_HIP_KIND_CAT(a, b) HCLIB_HIP_KIND_CAT2(a, b)
+#define HCLIB_HIP_DEVICE_ASYNC(fp, launcher)                                                        \
+    static const int HCLIB_HIP_KIND_CAT(hclib_hip_kind_reg_, __LINE__) =                            \
+        (hclib_hip_register_device_async((generic_frame_ptr)(fp), #fp, (launcher)), 0)
+#define HCLIB_HIP_DEVICE_FORASYNC(fct, launcher)                                                    \
+    static const int HCLIB_HIP_KIND_CAT(hclib_hip_body_reg_, __LINE__) =                            \
+        (hclib_hip_register_device_forasync((void *)(fct), #fct, (launcher)), 0)
+
+namespace hclib {
+namespace hip {
+
 // ------------------------------------------------------- device forasync
 struct RunTable {
     const hclib_sets::Run *runs;

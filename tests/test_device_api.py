@@ -73,3 +73,35 @@ def test_device_nested_finish_on_gpu():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Check results: OK" in r.stdout
     assert "fib(27) = 196418" in r.stdout and "nested finish: 100 iterations x 4" in r.stdout
+
+
+KT_EXE = os.path.join(os.path.dirname(H.LIB_PATH), "tests", "kind_table")
+
+
+def test_kind_table_program_is_built():
+    """tests/hip/kind_table.hip (device kinds of the program's own) linked
+    into the C program tests/c/kind_table_main.c."""
+    assert os.path.exists(KT_EXE), "run python -m hclib_amd.build"
+
+
+def test_kind_table_refuses_unknown_builtin_kinds():
+    """A kind id outside the table is refused, naming the way to register a
+    kind of the program's own (no GPU needed: it fails before any launch)."""
+    r = subprocess.run([KT_EXE, "bad"], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "unknown kind 99" in r.stderr and "hclib_hip_register_device_async" in r.stderr
+    assert "accepted" not in r.stdout
+
+
+@pytest.mark.gpu
+def test_kind_table_device_kinds_from_the_programs_hip_object():
+    """The C drop-in runs hclib_async(fib, ...) through the program's own
+    device kind (nested-finish fib on the megakernel) and hclib_forasync of
+    the program's own device loop body over GPU-locale memory (FLAT and
+    RECURSIVE), both checked against host evaluation."""
+    r = subprocess.run([KT_EXE], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Check results: OK" in r.stdout
+    assert "Fib(25) = 75025 = 75025" in r.stdout
+    assert "forasync (FLAT) of the device body: 100000 indices OK" in r.stdout
+    assert "forasync (RECURSIVE) of the device body: 100000 indices OK" in r.stdout
