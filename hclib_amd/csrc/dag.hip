@@ -122,7 +122,7 @@ extern "C" int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t
         g_dag.arena_bytes = bytes;
     }
     char *d = (char *)g_dag.arena;
-    HX_HIP(hipMemcpyAsync(d, h.data(), bytes, hipMemcpyHostToDevice, m.stream));
+    HX_TRY(upload_async(d, h.data(), bytes, m.stream));
     DagView &v = g_dag.view;
     v.head = (uint32_t *)(d + o_ctl);
     v.tail = (uint32_t *)(d + o_ctl + 256);
@@ -206,6 +206,164 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
     if (st[0] != g_dag.ntasks) {
         set_error("%s: %llu of %u tasks ran", w, (unsigned long long)st[0], g_dag.ntasks);
         return HCLIB_HIP_EDEVICE;
+    }
+    return HCLIB_HIP_OK;
+}
+
+// ------------------------------------------------ dynamic device dataflow
+// (include/hclib_hip/hx_dyn.h) — the host half: pools, the roots, the
+// launch's end. Promise heads start kDynOpen (0xff bytes), the ready list
+// kDynEmpty; the roots take ready slots 0 .. nroots - 1 with no pending
+// futures, and `live` starts at nroots.
+#include "../../include/hclib_hip/hx_dyn.h"
+
+namespace hx {
+namespace {
+struct DynState {
+    bool active = false;
+    DynView view{};
+    void *arena = nullptr;
+    size_t arena_bytes = 0;
+};
+DynState g_dyn;
+}  // namespace
+}  // namespace hx
+
+extern "C" int hclib_hip_dyn_begin(uint32_t payload_words, const uint32_t *root_payload, uint32_t nroots,
+                                   uint32_t task_cap, uint32_t promise_cap, uint32_t node_cap, int waves_per_cu,
+                                   uint32_t spin_limit_ms, hclib_hip_dyn_launch_t *out) {
+    if (!out || payload_words > (uint32_t)kDynMaxPayload || nroots == 0 || nroots > task_cap ||
+        (payload_words && !root_payload) || task_cap >= kDynPut || promise_cap >= kDynPut || node_cap >= kDynPut ||
+        waves_per_cu < 1 || waves_per_cu > 8) {
+        set_error("hclib_hip_dyn_begin: invalid arguments (1 <= nroots <= task_cap, payload_words <= %d, "
+                  "1..8 waves per CU)", kDynMaxPayload);
+        return HCLIB_HIP_EINVAL;
+    }
+    if (g_dyn.active) {
+        set_error("hclib_hip_dyn_begin: a dynamic launch is already open (call hclib_hip_dyn_end)");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    Module &m = mod();
+    const int64_t grid = (int64_t)m.num_cus * waves_per_cu;
+    const uint32_t rcap = task_cap + (uint32_t)grid + 64;
+    const uint32_t pcap = promise_cap ? promise_cap : 1, wcap = node_cap ? node_cap : 1;
+    const size_t o_ctl = 0, o_stats = 2048, o_datum = 2304;
+    const size_t o_phead = o_datum + up256((size_t)pcap * 8);
+    const size_t o_wtask = o_phead + up256((size_t)pcap * 4);
+    const size_t o_wnext = o_wtask + up256((size_t)wcap * 4);
+    const size_t o_tdeps = o_wnext + up256((size_t)wcap * 4);
+    const size_t o_tpay = o_tdeps + up256((size_t)task_cap * 4);
+    const size_t o_ready = o_tpay + up256((size_t)task_cap * payload_words * 4 + 4);
+    const size_t bytes = o_ready + up256((size_t)rcap * 4);
+    if (bytes > g_dyn.arena_bytes) {
+        if (g_dyn.arena) (void)hipFree(g_dyn.arena);
+        g_dyn.arena = nullptr;
+        g_dyn.arena_bytes = 0;
+        if (hipMalloc(&g_dyn.arena, bytes) != hipSuccess) {
+            set_error("hclib_hip_dyn_begin: hipMalloc(%zu) failed", bytes);
+            return HCLIB_HIP_ENOMEM;
+        }
+        g_dyn.arena_bytes = bytes;
+    }
+    char *d = (char *)g_dyn.arena;
+    // control + stats zeroed, heads and ready slots 0xff, then the roots
+    HX_HIP(hipMemsetAsync(d, 0, o_datum, m.stream));
+    HX_HIP(hipMemsetAsync(d + o_phead, 0xff, (size_t)pcap * 4, m.stream));
+    HX_HIP(hipMemsetAsync(d + o_tdeps, 0, (size_t)task_cap * 4, m.stream));
+    HX_HIP(hipMemsetAsync(d + o_ready, 0xff, (size_t)rcap * 4, m.stream));
+    std::vector<uint32_t> ctl(2048 / 4, 0), ready(nroots);
+    ctl[64] = nroots;   // tail
+    ctl[128] = nroots;  // live
+    ctl[256] = nroots;  // next task id
+    for (uint32_t r = 0; r < nroots; ++r) ready[r] = r;
+    HX_TRY(upload_async(d + o_ctl, ctl.data(), 2048, m.stream));
+    HX_TRY(upload_async(d + o_ready, ready.data(), (size_t)nroots * 4, m.stream));
+    if (payload_words) HX_TRY(upload_async(d + o_tpay, root_payload, (size_t)nroots * payload_words * 4, m.stream));
+    DynView &v = g_dyn.view;
+    v.ctl = (uint32_t *)(d + o_ctl);
+    v.stats = (unsigned long long *)(d + o_stats);
+    v.datum = (unsigned long long *)(d + o_datum);
+    v.phead = (uint32_t *)(d + o_phead);
+    v.wtask = (uint32_t *)(d + o_wtask);
+    v.wnext = (uint32_t *)(d + o_wnext);
+    v.tdeps = (uint32_t *)(d + o_tdeps);
+    v.tpay = (uint32_t *)(d + o_tpay);
+    v.ready = (uint32_t *)(d + o_ready);
+    v.tcap = task_cap;
+    v.pcap = promise_cap;
+    v.wcap = node_cap;
+    v.rcap = rcap;
+    v.payload_words = payload_words;
+    v.spin_ms = spin_limit_ms ? spin_limit_ms : (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
+    g_dyn.active = true;
+    HX_HIP(hipEventRecord(m.ev0, m.stream));
+    out->view = &g_dyn.view;
+    out->stream = m.stream;
+    out->grid = (int)grid;
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_dyn_end(const char *who, hclib_hip_dyn_stats_t *stats) {
+    if (!g_dyn.active) {
+        set_error("hclib_hip_dyn_end: no open dynamic launch");
+        return HCLIB_HIP_EINVAL;
+    }
+    g_dyn.active = false;
+    Module &m = mod();
+    const DynView &v = g_dyn.view;
+    HX_HIP(hipGetLastError());
+    HX_HIP(hipEventRecord(m.ev1, m.stream));
+    uint32_t ctl[512];
+    unsigned long long st[5] = {0, 0, 0, 0, 0};
+    HX_HIP(hipMemcpyAsync(ctl, v.ctl, sizeof(ctl), hipMemcpyDeviceToHost, m.stream));
+    HX_HIP(hipMemcpyAsync(st, v.stats, sizeof(st), hipMemcpyDeviceToHost, m.stream));
+    HX_HIP(hipStreamSynchronize(m.stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
+    if (stats) {
+        stats->tasks = st[0];
+        stats->puts = st[1];
+        stats->created = st[2];
+        stats->releases = st[3];
+        stats->promises = st[4];
+        stats->kernel_ms = ms;
+    }
+    const char *w = who ? who : "hclib_hip_dyn";
+    const uint32_t err = ctl[192], live = ctl[128];
+    if (err == kErrDynDoublePut) {
+        set_error("%s: violated single assignment property for promises (device put on a satisfied promise)", w);
+        return HCLIB_HIP_EDEVICE;
+    }
+    if (err == kErrDynPool) {
+        set_error("%s: a device pool ran out (tasks %u/%u, promises %u/%u, wait nodes %u/%u)", w, ctl[256], v.tcap,
+                  ctl[320], v.pcap, ctl[384], v.wcap);
+        return HCLIB_HIP_EDEVICE;
+    }
+    if (err == kErrSpinTimeout || (!err && live)) {
+        set_error("%s: %llu task(s) ran, %u still wait on promises that nothing puts (deadlock)", w,
+                  (unsigned long long)st[0], live);
+        return HCLIB_HIP_EDEVICE;
+    }
+    if (err) {
+        set_error("%s: device error %u", w, err);
+        return HCLIB_HIP_EDEVICE;
+    }
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_dyn_datum(uint32_t first, uint32_t n, uint64_t *datum, uint8_t *put) {
+    const DynView &v = g_dyn.view;
+    if (g_dyn.active || !g_dyn.arena || (uint64_t)first + n > v.pcap) {
+        set_error("hclib_hip_dyn_datum: no finished launch or promises [%u, %u) outside the pool", first, first + n);
+        return HCLIB_HIP_EINVAL;
+    }
+    if (!n) return HCLIB_HIP_OK;
+    if (datum) HX_HIP(hipMemcpy(datum, v.datum + first, (size_t)n * 8, hipMemcpyDeviceToHost));
+    if (put) {
+        std::vector<uint32_t> h(n);
+        HX_HIP(hipMemcpy(h.data(), v.phead + first, (size_t)n * 4, hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < n; ++k) put[k] = h[k] == kDynPut ? 1 : 0;
     }
     return HCLIB_HIP_OK;
 }

@@ -273,6 +273,7 @@ __global__ __launch_bounds__(256) void k_forasync_sweep(SweepArgs A) {
 }
 
 // -------------------------------------------------- host: iteration sets
+
 // include/hclib_forasync_sets.h (shared with the C++ layers)
 static std::vector<Run> dim_runs(const hclib_hip_loop_domain_t &d, int ndim, int mode) {
     const hclib_sets::Domain dd{d.low, d.high, d.stride, d.tile};
@@ -368,7 +369,7 @@ extern "C" int hclib_hip_forasync_plan(int dim, hclib_hip_loop_domain_t *domain,
         off += (pre[d].size() * 8 + 15) & ~(size_t)15;
         plan->nruns[d] = (int)runs[d].size();
     }
-    HX_HIP(hipMemcpyAsync(dbuf, hbuf.data(), bytes, hipMemcpyHostToDevice, st));
+    HX_TRY(upload_async(dbuf, hbuf.data(), bytes, st));
     plan->mem = dbuf;
     return HCLIB_HIP_OK;
 }
@@ -444,8 +445,7 @@ extern "C" int hclib_hip_forasync(int body, const void *args, int dim,
         off += (pre[d].size() * 8 + 15) & ~(size_t)15;
         A.dim[d].nruns = (int)runs[d].size();
     }
-    // pageable source: the copy has consumed hbuf when it returns
-    HX_HIP(hipMemcpyAsync(dbuf, hbuf.data(), bytes, hipMemcpyHostToDevice, st));
+    HX_TRY(upload_async(dbuf, hbuf.data(), bytes, st));
     int64_t grid = (A.total + 255) / 256;
     const int64_t maxg = (int64_t)mod().num_cus * 16;
     if (grid > maxg) grid = maxg;

@@ -37,6 +37,9 @@ Module &mod();
 void set_error(const char *fmt, ...);
 int ensure_device();  // HCLIB_HIP_OK or HCLIB_HIP_ENODEV
 int hip_check(hipError_t e, const char *what);
+// host -> device copy of `bytes` at `src` in `stream` order through a pinned
+// staging buffer: `src` may be freed as soon as the call returns
+int upload_async(void *dst, const void *src, size_t bytes, hipStream_t stream);
 
 // Carve a PoolView for `words` u32 per entry out of the arena (grows it).
 int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolView *out);

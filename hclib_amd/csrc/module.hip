@@ -77,6 +77,57 @@ int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolVie
     return HCLIB_HIP_OK;
 }
 
+// Host -> device copies of temporaries travel through pinned staging
+// buffers: an asynchronous copy from pageable memory may read its source
+// after the call returns (observed: a forasync sweep reading a stale run
+// table from stream-ordered memory), so the source must live until the
+// copy is done. Each buffer is freed once the event recorded
+// after its copy has completed (checked on every upload).
+struct Staged {
+    void *host;
+    hipEvent_t done;
+};
+std::vector<Staged> &staged() {
+    static std::vector<Staged> v;
+    return v;
+}
+void reap_staged() {
+    std::vector<Staged> &v = staged();
+    for (size_t i = 0; i < v.size();) {
+        if (hipEventQuery(v[i].done) == hipSuccess) {
+            (void)hipHostFree(v[i].host);
+            (void)hipEventDestroy(v[i].done);
+            v[i] = v.back();
+            v.pop_back();
+        } else {
+            ++i;
+        }
+    }
+}
+// copy `bytes` of `src` to device `dst` in `st` order; src may be freed on return
+int upload_async(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    reap_staged();
+    void *pin = nullptr;
+    HX_HIP(hipHostMalloc(&pin, bytes, hipHostMallocDefault));
+    memcpy(pin, src, bytes);
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipHostFree(pin);
+        set_error("upload: hipEventCreate failed");
+        return HCLIB_HIP_EHIP;
+    }
+    if (hipMemcpyAsync(dst, pin, bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipEventRecord(ev, st) != hipSuccess) {
+        (void)hipStreamSynchronize(st);
+        (void)hipHostFree(pin);
+        (void)hipEventDestroy(ev);
+        set_error("upload: host-to-device copy failed");
+        return HCLIB_HIP_EHIP;
+    }
+    staged().push_back(Staged{pin, ev});
+    return HCLIB_HIP_OK;
+}
+
 int reset_sched(const PoolView &pool, uint32_t outstanding_init) {
     Module &m = g_mod;
     HX_HIP(hipMemsetAsync(pool.hdr, 0, sizeof(QueueHdr) * pool.nq, m.stream));
@@ -89,7 +140,13 @@ int reset_sched(const PoolView &pool, uint32_t outstanding_init) {
     init.outstanding = outstanding_init;
     init.wave_stats = m.wave_stats;
     init.wave_stats_cap = m.wave_stats_cap;
-    HX_HIP(hipMemcpyAsync(m.globals, &init, sizeof(init), hipMemcpyHostToDevice, m.stream));
+    // a pinned staging copy of its own, reused: every launch ends with the
+    // stream synchronised (hclib_hip_sched_end), so the last copy is done
+    static SchedGlobals *stage = nullptr;
+    if (!stage && hipHostMalloc((void **)&stage, sizeof(SchedGlobals), hipHostMallocDefault) != hipSuccess)
+        return upload_async(m.globals, &init, sizeof(init), m.stream);
+    *stage = init;
+    HX_HIP(hipMemcpyAsync(m.globals, stage, sizeof(init), hipMemcpyHostToDevice, m.stream));
     return HCLIB_HIP_OK;
 }
 

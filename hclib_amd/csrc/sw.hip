@@ -572,8 +572,8 @@ inline bool sw_band_ok(int th, int bh) { return th % bh == 0 && th / bh >= 1 && 
 // per lane need th % 128 == 0, else one row per lane with the same hand-off
 inline int sw_pick_form(int th, int def) {
     int form = env_int("HCLIB_HIP_SW_FORM", def);
-    if (form != 11 && form != 12 && form != 21 && form != 22 && form != 211 && form != 212 && form != 214 &&
-        form != 411 && form != 412 && form != 414)
+    if (form != 11 && form != 12 && form != 14 && form != 21 && form != 22 && form != 211 && form != 212 &&
+        form != 214 && form != 411 && form != 412 && form != 414)
         form = def;
     if (form > 400 && th % 256 != 0) form -= 200;
     if (form > 200 && th % 128 != 0) form -= 200;
@@ -1003,6 +1003,7 @@ __device__ __forceinline__ bool sw_band_row_any(int form, const SwCtx &c, const 
     switch (form) {
         case 11: return sw_band_row<1, 16, 1>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
         case 12: return sw_band_row<1, 32, 1>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
+        case 14: return sw_band_row<1, 64, 1>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
         case 21: return sw_band_row<2, 16, 1>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
         case 22: return sw_band_row<2, 32, 1>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
         case 211: return sw_band_row<1, 16, 2>(c, B, w, rings, dummy, code_rings, prod, cons, ph, stamp_first);
@@ -1212,8 +1213,11 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     // for the one-wave-per-tile-row kernel
     // multi-wave band form (sw_pick_form): the DAG's tile tasks default to two
     // rows per lane (two waves per 256-row tile: one hand-off lag instead of
-    // three), the row schedule to one
-    const int form = sw_pick_form(th, dag ? 212 : 12), bh = sw_form_bh(form);
+    // three), the row schedule to four (one band per 256-row tile row: the
+    // per-row wavefront lag is paid once per 256 rows). SW-64K measured
+    // (profiles/r02/sw_forms.log): rows 12: 4.4 ms, 212: 3.55, 412: 3.50;
+    // dag 12: 11.2, 212: 9.4, 412: 9.6
+    const int form = sw_pick_form(th, dag ? 212 : 412), bh = sw_form_bh(form);
     const bool band_shape = sw_band_ok(th, bh) && tw <= 65536;
     const bool band = rows && band_shape && !(sched && !strcmp(sched, "rows1"));
     const size_t nt = ntw * nth;
@@ -1454,7 +1458,7 @@ extern "C" int hclib_hip_sw_band_begin(const int8_t *s1, size_t n1, const int8_t
     c.j0 = j0;
     c.j1 = j1;
     c.progressive = env_int("HCLIB_HIP_SW_PROGRESSIVE", 1);
-    c.form = sw_pick_form(th, 12);
+    c.form = sw_pick_form(th, 412);
     c.bh = sw_form_bh(c.form);
     c.spin_ms = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     h->lds = lds;

@@ -309,6 +309,41 @@ int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t payload_wo
 int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *satisfied_out,
                       hclib_hip_dag_stats_t *stats);
 
+/* ------------------------------------------ dynamic device dataflow */
+/* Device tasks that create promises and async_await tasks while the launch
+ * runs (include/hclib_hip/hx_dyn.h; hclib_promise_create / put and
+ * spawn_await of src/hclib-promise.c:55-245, src/hclib-runtime.c:596-644 as
+ * running tasks use them). begin() allocates the pools — task_cap tasks of
+ * payload_words u32 each, promise_cap promises, node_cap wait nodes (one per
+ * registered future) — seeds the ready list with the `nroots` root tasks
+ * (payloads in root_payload) and records the start event; the caller
+ * launches `grid` workgroups of 64 threads on `stream` running
+ * hx::run_dyn_worker<Kind> over `view` (hclib::hip::run_dyn does both);
+ * end() waits and returns HCLIB_HIP_EDEVICE for a double put, an exhausted
+ * pool or tasks that wait on promises nothing puts (bounded spin, the
+ * reference's end_finish deadlock). datum() then reads promises back. */
+typedef struct {
+    void *view;    /* hx::DynView (device pointers, by value) */
+    void *stream;  /* hipStream_t of the module */
+    int grid;      /* workgroups (waves) to launch */
+} hclib_hip_dyn_launch_t;
+
+typedef struct {
+    uint64_t tasks;     /* tasks run (roots included) */
+    uint64_t created;   /* tasks created by device async_await */
+    uint64_t puts;      /* device puts */
+    uint64_t releases;  /* waiters a put made runnable */
+    uint64_t promises;  /* promises created on the device */
+    double kernel_ms;
+} hclib_hip_dyn_stats_t;
+
+int hclib_hip_dyn_begin(uint32_t payload_words, const uint32_t *root_payload, uint32_t nroots, uint32_t task_cap,
+                        uint32_t promise_cap, uint32_t node_cap, int waves_per_cu, uint32_t spin_limit_ms,
+                        hclib_hip_dyn_launch_t *out);
+int hclib_hip_dyn_end(const char *who, hclib_hip_dyn_stats_t *stats);
+/* promises [first, first + n) of the last launch: data, and whether put */
+int hclib_hip_dyn_datum(uint32_t first, uint32_t n, uint64_t *datum, uint8_t *put);
+
 /* ---------------------------------------------------------------- SW */
 typedef struct {
     uint64_t tiles;      /* tile tasks executed */

@@ -50,6 +50,7 @@
 #include "hclib_cpp.h"
 #include "hclib_hip.h"
 #include "hclib_hip/hx_dag.h"
+#include "hclib_hip/hx_dyn.h"
 #include "hclib_hip/hx_finish.h"
 #include "hclib_hip/hx_sched.h"
 
@@ -459,6 +460,44 @@ int run_dag(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats,
     g.sat_.assign(g.num_promises(), 0);
     hclib_hip_dag_stats_t local;
     return hclib_hip_dag_end("hclib::hip::run_dag", g.datum_.data(), g.sat_.data(), stats ? stats : &local);
+}
+
+// ------------------------------------------------- dynamic device dataflow
+// run_dyn<Kind>(ctx, roots, caps): the root tasks (payload_words u32 each,
+// `roots` holds nroots * payload_words words) run on the persistent waves
+// and create promises and async_await tasks as they go
+// (include/hclib_hip/hx_dyn.h); returns when every created task has run, or
+// HCLIB_HIP_EDEVICE (double put, pool exhausted, deadlock). dyn_datum reads
+// promises back afterwards.
+struct dyn_caps {
+    uint32_t tasks = 1u << 20, promises = 1u << 20, wait_nodes = 1u << 21;
+    int waves_per_cu = 4;
+    uint32_t spin_limit_ms = 0;  // 0: HCLIB_HIP_SPIN_LIMIT_MS or 20 s
+};
+
+template <class Kind>
+__global__ __launch_bounds__(64) void k_run_dyn(typename Kind::Ctx ctx, hx::DynView v) {
+    hx::run_dyn_worker<Kind>(ctx, v);
+}
+
+template <class Kind>
+int run_dyn(const typename Kind::Ctx &ctx, uint32_t payload_words, const std::vector<uint32_t> &roots,
+            const dyn_caps &caps = dyn_caps(), hclib_hip_dyn_stats_t *stats = nullptr) {
+    const uint32_t nroots = payload_words ? (uint32_t)(roots.size() / payload_words) : (uint32_t)roots.size();
+    hclib_hip_dyn_launch_t L;
+    int rc = hclib_hip_dyn_begin(payload_words, roots.data(), nroots, caps.tasks, caps.promises, caps.wait_nodes,
+                                 caps.waves_per_cu, caps.spin_limit_ms, &L);
+    if (rc != HCLIB_HIP_OK) return rc;
+    const hx::DynView v = *(const hx::DynView *)L.view;
+    hipLaunchKernelGGL((k_run_dyn<Kind>), dim3(L.grid), dim3(64), 0, (hipStream_t)L.stream, ctx, v);
+    hclib_hip_dyn_stats_t local;
+    return hclib_hip_dyn_end("hclib::hip::run_dyn", stats ? stats : &local);
+}
+
+inline std::vector<uint64_t> dyn_datum(uint32_t first, uint32_t n) {
+    std::vector<uint64_t> d(n, 0);
+    if (hclib_hip_dyn_datum(first, n, d.data(), nullptr) != HCLIB_HIP_OK) d.clear();
+    return d;
 }
 
 }  // namespace hip

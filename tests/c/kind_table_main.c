@@ -76,7 +76,9 @@ static void entry(void *unused) {
     int *dx = hclib_future_wait(hclib_allocate_at(N * sizeof(int), gpu));
     int *dy = hclib_future_wait(hclib_allocate_at(N * sizeof(int), gpu));
     hclib_future_wait(hclib_async_copy(gpu, dx, host, hx, N * sizeof(int), NULL, 0));
-    for (int mode = 0; mode < 2; ++mode) {
+    const int reps = getenv("KIND_TABLE_REPS") ? atoi(getenv("KIND_TABLE_REPS")) : 1;
+    for (int it = 0; it < 2 * reps; ++it) {
+        const int mode = it % 2;
         hclib_future_wait(hclib_memset_at(dy, 0, N * sizeof(int), gpu));
         ScaleArgs sa = {dy, dx};
         hclib_loop_domain_t dom = {0, N, 1, -1};
@@ -84,11 +86,18 @@ static void entry(void *unused) {
         hclib_forasync(scale_body, &sa, 1, &dom, mode == 0 ? FORASYNC_MODE_FLAT : FORASYNC_MODE_RECURSIVE);
         hclib_end_finish();
         hclib_future_wait(hclib_async_copy(host, hy, gpu, dy, N * sizeof(int), NULL, 0));
+        int bad = 0, first_bad = -1, last_bad = -1;
         for (int i = 0; i < N; ++i)
             if (hy[i] != 3 * hx[i] + i) {
-                fprintf(stderr, "mode %d: y[%d] = %d, want %d\n", mode, i, hy[i], 3 * hx[i] + i);
-                exit(1);
+                if (first_bad < 0) first_bad = i;
+                last_bad = i;
+                ++bad;
             }
+        if (bad) {
+            fprintf(stderr, "mode %d: %d wrong indices in [%d, %d]; y[%d] = %d, want %d (tile %d)\n", mode, bad,
+                    first_bad, last_bad, first_bad, hy[first_bad], 3 * hx[first_bad] + first_bad, dom.tile);
+            exit(1);
+        }
         printf("forasync (%s) of the device body: %d indices OK\n", mode == 0 ? "FLAT" : "RECURSIVE", N);
     }
     hclib_free_at(dx, gpu);

@@ -105,3 +105,26 @@ def test_kind_table_device_kinds_from_the_programs_hip_object():
     assert "Fib(25) = 75025 = 75025" in r.stdout
     assert "forasync (FLAT) of the device body: 100000 indices OK" in r.stdout
     assert "forasync (RECURSIVE) of the device body: 100000 indices OK" in r.stdout
+
+
+DYN_EXE = os.path.join(os.path.dirname(H.LIB_PATH), "tests", "device_dyn")
+
+
+def test_device_dyn_program_is_built():
+    assert os.path.exists(DYN_EXE), "run python -m hclib_amd.build"
+
+
+@pytest.mark.gpu
+def test_dynamic_device_dataflow_on_gpu():
+    """Device tasks that create promises and async_await tasks while the
+    launch runs (include/hclib_hip/hx_dyn.h): fib with data-driven tasks
+    (test/fib/fib.c:113-141) for n = 0..22 with the exact task / promise /
+    put counts, the smith_waterman.cpp:171-232 tile program (a root task
+    creating 3 promises and one async_await per tile) against a serial host
+    DP, and a double put / a never-put future returning HCLIB_HIP_EDEVICE."""
+    r = subprocess.run([DYN_EXE], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Check results: OK" in r.stdout
+    assert "fib(22) = 17711 with data-driven device tasks" in r.stdout
+    assert "as device async_awaits: score" in r.stdout
+    assert "single assignment" in r.stdout and "deadlock" in r.stdout

@@ -337,7 +337,7 @@ def test_sw_multiwave_tile_rows(n1, n2, tw, th, monkeypatch):
     s2 = bytes(rng.integers(1, 5, n2, dtype=np.int8).tobytes())
     want = L.sw_score(s1, s2, tw, th)
     # every (rows per lane, skew, hand-off) form: 100 R + 10 S + K / 16
-    for form in ("11", "12", "21", "22", "211", "212", "214", "411", "412", "414"):
+    for form in ("11", "12", "14", "21", "22", "211", "212", "214", "411", "412", "414"):
         monkeypatch.setenv("HCLIB_HIP_SW_FORM", form)
         score, st = H.sw(s1, s2, tw, th)
         assert score == want and st["tiles"] == (n1 // tw) * (n2 // th), form
