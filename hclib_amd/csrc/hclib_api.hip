@@ -339,7 +339,9 @@ void add_device_op(hipStream_t stream, void (*done)(void *), void *arg) {
 // the newest ready task; with nothing ready, wait for the oldest device work
 bool run_one() {
     Runtime &R = rt();
-    poll_pending(false);
+    // an operation completed here may have put the promise the caller waits
+    // on: that is progress, even with nothing left to run or wait for
+    if (poll_pending(false) && R.ready.empty()) return true;
     if (R.ready.empty()) return poll_pending(true);
     hclib_task_t *t = R.ready.back();
     R.ready.pop_back();

@@ -71,6 +71,15 @@ __device__ __forceinline__ void acquire_agent() {
 }
 
 // ------------------------------------------------------------ wave utils
+// hclib_get_current_worker / hclib_get_num_workers in device code
+// (src/hclib-runtime.c:194-226): a device worker is one wave of the launch,
+// numbered 0 .. num_workers() - 1 across the grid (UTS.cpp:104-106,220-221
+// index per-worker state by it)
+__device__ __forceinline__ int current_worker() {
+    return (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+}
+__device__ __forceinline__ int num_workers() { return (int)(gridDim.x * (blockDim.x >> 6)); }
+
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // XCD (XCC) id of the executing CU: speed hint only, never correctness.

@@ -100,6 +100,29 @@ static void entry(void *unused) {
         }
         printf("forasync (%s) of the device body: %d indices OK\n", mode == 0 ? "FLAT" : "RECURSIVE", N);
     }
+    /* R4 with device work (src/hclib.c:466-473, src/hclib-runtime.c:1280-1313):
+     * forasync_future of the device body and a non-blocking finish around a
+     * device task return futures at once; the host waits on them later */
+    {
+        hclib_future_wait(hclib_memset_at(dy, 0, N * sizeof(int), gpu));
+        ScaleArgs sa = {dy, dx};
+        hclib_loop_domain_t dom = {0, N, 1, -1};
+        hclib_future_t *f = hclib_forasync_future(scale_body, &sa, 1, &dom, FORASYNC_MODE_RECURSIVE);
+        FibArgs args = {20, -1};
+        hclib_start_finish();
+        hclib_async(fib, &args, NULL, 0, hclib_hip_gpu_locale(0));
+        hclib_future_t *g = hclib_end_finish_nonblocking();
+        hclib_future_wait(g);
+        hclib_future_wait(f);
+        hclib_future_wait(hclib_async_copy(host, hy, gpu, dy, N * sizeof(int), NULL, 0));
+        for (int i = 0; i < N; ++i)
+            if (hy[i] != 3 * hx[i] + i) {
+                fprintf(stderr, "forasync_future: y[%d] = %d, want %d\n", i, hy[i], 3 * hx[i] + i);
+                exit(1);
+            }
+        assert(args.res == fib_iter(20));
+        printf("forasync_future + end_finish_nonblocking with device work: OK\n");
+    }
     hclib_free_at(dx, gpu);
     hclib_free_at(dy, gpu);
     free(hx);

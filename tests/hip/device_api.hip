@@ -173,6 +173,42 @@ struct QueensKind {
     }
 };
 
+// ------------------------------------------- worker identity in a kind
+// UTS.cpp:104-106,220-221 keep per-worker state indexed by
+// hclib_get_current_worker(): here every task adds itself to its worker's
+// tally (hx::current_worker(), one wave = one worker)
+struct WorkerCtx {
+    int n;
+    unsigned int *tally;  // [num_workers]
+    unsigned int *bad;    // ids outside [0, num_workers)
+};
+struct WorkerKind {
+    static constexpr int kTmplWords = 2;
+    static constexpr int kWords = 4;
+    static constexpr bool kPure = false;  // the tallies are side effects
+    static constexpr bool kBoundedChildren = true;
+    using Ctx = WorkerCtx;
+    struct Acc {
+        __device__ void flush(hx::SchedGlobals *) {}
+    };
+    __device__ static int roots(const Ctx &c, Acc &, uint32_t *t) {
+        t[0] = (uint32_t)c.n + 1;
+        t[1] = 0;
+        return 1;
+    }
+    __device__ static int process(const Ctx &c, Acc &, const uint32_t *t, uint32_t k, uint32_t *child, uint32_t *,
+                                  bool) {
+        const int w = hx::current_worker(), nw = hx::num_workers();
+        if (w < 0 || w >= nw) atomicAdd(c.bad, 1u);
+        else atomicAdd(&c.tally[w], 1u);
+        const int m = (int)t[0] - 1 - (int)k;
+        if (m < 2) return 0;
+        child[0] = (uint32_t)m;
+        child[1] = 0;
+        return 2;
+    }
+};
+
 static void host_queens(int n, int row, uint32_t cols, uint32_t ld, uint32_t rd, unsigned long long &sols,
                         unsigned long long &nodes) {
     const uint32_t mask = (1u << n) - 1u;
@@ -227,6 +263,33 @@ int main() {
         CHECK(st.counters[0] == sols && st.counters[1] == nodes, "queens(%d): %llu/%llu, want %llu/%llu", n,
               (unsigned long long)st.counters[0], (unsigned long long)st.counters[1], sols, nodes);
         if (n >= 10) printf("queens(%d) = %llu solutions, %llu placements (%.3f ms)\n", n, sols, nodes, st.kernel_ms);
+    }
+    // worker identity: every task tallied under a valid worker id, spread
+    // over many workers (fib(24): 150,049 tasks)
+    {
+        const int nw = hclib_hip_num_workers();
+        unsigned int *d = nullptr;
+        CHECK(nw > 0 && hipMalloc((void **)&d, (size_t)(nw + 1) * 4) == hipSuccess &&
+                  hipMemset(d, 0, (size_t)(nw + 1) * 4) == hipSuccess,
+              "tally buffer");
+        hclib::hip::task_config tc;
+        tc.spill_lo = 32;
+        hclib::hip::task_stats st;
+        int rc = hclib::hip::run_tasks<WorkerKind>(WorkerCtx{24, d, d + nw}, &st, tc);
+        CHECK(rc == HCLIB_HIP_OK, "run_tasks<WorkerKind>: %s", hclib_hip_last_error());
+        std::vector<unsigned int> h((size_t)nw + 1);
+        CHECK(hipMemcpy(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost) == hipSuccess, "copy tally");
+        unsigned long long total = 0;
+        int used = 0;
+        for (int w = 0; w < nw; ++w) {
+            total += h[w];
+            used += h[w] ? 1 : 0;
+        }
+        CHECK(h[nw] == 0, "%u tasks saw a worker id outside [0, %d)", h[nw], nw);
+        CHECK(total == 2 * 75025ull - 1, "tallied %llu tasks, want %llu", total, 2 * 75025ull - 1);
+        CHECK(used > 1, "only %d worker(s) ran tasks", used);
+        printf("worker identity: %llu tasks on %d of %d device workers\n", total, used, nw);
+        (void)hipFree(d);
     }
     printf("Check results: OK\n");
     return 0;

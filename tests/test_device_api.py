@@ -33,6 +33,7 @@ def test_device_api_on_gpu():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Check results: OK" in r.stdout
     assert "fib(25) = 75025" in r.stdout and "queens(12) = 14200 solutions" in r.stdout
+    assert "worker identity: 150049 tasks on" in r.stdout
 
 
 DAG_EXE = os.path.join(os.path.dirname(H.LIB_PATH), "tests", "device_dag")
@@ -105,6 +106,7 @@ def test_kind_table_device_kinds_from_the_programs_hip_object():
     assert "Fib(25) = 75025 = 75025" in r.stdout
     assert "forasync (FLAT) of the device body: 100000 indices OK" in r.stdout
     assert "forasync (RECURSIVE) of the device body: 100000 indices OK" in r.stdout
+    assert "forasync_future + end_finish_nonblocking with device work: OK" in r.stdout
 
 
 DYN_EXE = os.path.join(os.path.dirname(H.LIB_PATH), "tests", "device_dyn")
