@@ -754,6 +754,7 @@ struct SwBand {
     bool left_lds;       // leftcol points to LDS (plain loads)
     int *rightcol_lds;   // also keep the right column here
     int *corner_lds;     // H(R0, C0 + ncols): the right neighbour's corner
+    int *corner_out_lds = nullptr;  // the bottom row's last value, also here
 };
 
 // The workgroup's ingress wave: moves the top row into ring 0 and publishes
@@ -853,6 +854,7 @@ __device__ bool sw_band_egress(const SwCtx &c, const SwBand &B, int *ring, int *
             if (B.gout) st_agent(&B.gout[x], (1ull << 32) | (unsigned long long)(uint32_t)h);
             else st_agent(&B.hout[x], h);
             if (B.corner_out && x == ncols - 1) st_agent(B.corner_out, h);
+            if (B.corner_out_lds && x == ncols - 1) *B.corner_out_lds = h;
         }
         next = avail;
         if (lane == 0) lds_flag_st(&cons[nb], next);
@@ -1142,6 +1144,7 @@ struct SwDagWgKind {
         B.gout = nullptr;
         B.hout = c.bottom + (size_t)t * c.tw;
         B.corner_out = c.corner + t;
+        B.corner_out_lds = last + 3;  // the corner promise's datum (datums())
         __syncthreads();  // every wave has read `last`
         if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod[0..63], cons[0..63]
         if (threadIdx.x == 0) *last = (int)t;
@@ -1154,11 +1157,23 @@ struct SwDagWgKind {
             for (int q = 0; q < 6 && wave < 3; ++q) add_agent(&c.stats[4 + 6 * wave + q], ph[q]);
         return ok;
     }
-    // right column, bottom row, corner (:212-226): one release for all three
-    __device__ static void put(const SwCtx &c, DagWave &w, uint32_t t) {
-        const uint32_t ps[3] = {3u * t + 0u, 3u * t + 1u, 3u * t + 2u};
-        const unsigned long long ds[3] = {0ull, 0ull, (unsigned long long)(uint32_t)ld_agent(&c.corner[t])};
-        dag_put_n<3, true>(w, ps, ds);
+    // right column, bottom row, corner (:212-226): run_dag_group's split put
+    // (waiters prefetched while the tile runs, one release for all three)
+    static constexpr int kPutN = 3;
+    __device__ static void promises(const SwCtx &, uint32_t t, uint32_t (&p)[3]) {
+        p[0] = 3u * t + 0u;
+        p[1] = 3u * t + 1u;
+        p[2] = 3u * t + 2u;
+    }
+    __device__ static void datums(const SwCtx &c, uint32_t t, unsigned long long (&d)[3]) {
+        extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+        const int nw = c.th / c.bh;
+        const int *last = (const int *)((const uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * 128) +
+                                        nw * 2048) + 128;
+        (void)t;
+        d[0] = 0ull;
+        d[1] = 0ull;
+        d[2] = (unsigned long long)(uint32_t)last[3];  // the egress wave's copy of c.corner[t]
     }
 };
 

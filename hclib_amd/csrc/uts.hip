@@ -628,6 +628,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // hunger read every 32 batches, every 8 while many waves are hungry
     // (scripts/sweep_uts.py: T1 1.37 -> 1.07 ms, T1XL 101 -> 97 ms, T3L even)
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", 32);
+    cfg.hunger_fast = (uint32_t)env_int("HCLIB_HIP_HUNGER_FAST", 0);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
     cfg.backoff = (uint32_t)env_int("HCLIB_HIP_BACKOFF", 16);
     HX_TRY(reset_sched(pool, 1));

@@ -303,10 +303,48 @@ __device__ void run_dag_worker(const typename Kind::Ctx &ctx, const DagView &vie
 // Concept additions: run_group and put as above, and kSc1Payload: true when
 // the bodies read what other tasks wrote only with agent-scope (sc1) loads,
 // so no acquire fence (an L2 invalidate) is needed before a body.
+// A Kind of run_dag_group may declare its puts up front —
+//   static constexpr int kPutN;  // promises every task puts, 1..64
+//   static void promises(const Ctx&, uint32_t task, uint32_t (&p)[kPutN]);
+//   static void datums(const Ctx&, uint32_t task, unsigned long long (&d)[kPutN]);
+// — in place of put(): the put is then split around the task (see below).
+template <class K, class = void>
+struct group_put_n { static constexpr int value = 0; };
+template <class K>
+struct group_put_n<K, decltype((void)K::kPutN)> { static constexpr int value = K::kPutN; };
+
+// State the waves of one workgroup share across its tasks (LDS).
+struct DagGroupShared {
+    uint32_t slot;        // the task wave 0 found
+    uint32_t nwait;       // waiters of the running task's promises (> 64: not prefetched)
+    uint32_t npend;       // tasks the last put released for the ready list
+    uint32_t skip;        // 1: the last put kept a task (its ready slot is a skip)
+    uint32_t dbl;         // the running task put a promise twice
+    uint32_t waiter[64];  // their ids, concatenated in promise order
+    uint32_t pend[64];
+};
+
+// The workgroup form of run_dag_worker: one task at a time, every wave of the
+// workgroup in Kind::run_group (a band of the tile each, an ingress and an
+// egress wave, ...). Wave 0 takes tickets and puts. With kPutN the put is
+// split so that one memory round trip past the task's own drain stays on the
+// chain from a task to its successor:
+//   * while the task runs, the last wave loads the waiter lists of its
+//     promises (static: the CSR the host built) into LDS;
+//   * at its end the same wave stores the datums and marks the promises
+//     satisfied behind the drain of its own outputs; after the task's barrier
+//     wave 0 decrements the waiters' counters, keeps one released task and
+//     leaves the others in LDS;
+//   * the last wave appends those (and the kept task's skip) to the ready
+//     list while wave 0 is already looking for the next task.
 template <class Kind>
-__device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view, uint32_t *slot) {
+__device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view, uint32_t *slot_unused) {
+    (void)slot_unused;
+    constexpr int N = group_put_n<Kind>::value;
+    __shared__ DagGroupShared sh;
     DagWave w{view, 0, 0, kDagEmpty, 0, 0};
-    const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
+    const int lane = lane_id(), wave = (int)(threadIdx.x >> 6), nwaves = (int)(blockDim.x >> 6);
+    const int helper = nwaves - 1;
     unsigned long long ran = 0;
     // diagnostic build (HX_STAMPS): wave 0's cycles taking tasks / running
     // bodies / putting, into stats[3..5]
@@ -320,11 +358,27 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
         (void)k;
 #endif
     };
+    if (threadIdx.x == 0) {
+        sh.npend = 0;
+        sh.skip = 0;
+    }
+    __syncthreads();
     stamp(0);
     while (true) {
         bool kept = false;
         uint32_t pend_pos = 0;
         int pend_lane = 0;
+        if (N > 0 && wave == helper) {
+            // the previous put's releases: one tail fetch-add for all of them
+            const uint32_t np = sh.npend, sk = sh.skip;
+            if (np + sk) {
+                uint32_t base = 0;
+                if (lane == 0) base = add_agent(view.tail, np + sk);
+                base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
+                if ((uint32_t)lane < np) st_agent(&view.ready[base + (uint32_t)lane], sh.pend[lane]);
+                if (sk && lane == 0) st_agent(&view.ready[base + np], kDagSkip);
+            }
+        }
         if (wave == 0) {
             uint32_t t = kDagEmpty;
             while (true) {
@@ -359,21 +413,135 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
                 if (lane == 0) dev_error(view.err, kErrBadTask);
                 t = kDagEmpty;
             }
-            if (lane == 0) *slot = t;
+            if (lane == 0) sh.slot = t;
         }
         __syncthreads();
-        const uint32_t t = *slot;
+        const uint32_t t = sh.slot;
         __syncthreads();  // the slot is rewritten only after this barrier
         if (t == kDagEmpty) break;
         if (!Kind::kSc1Payload) acquire_agent();
         stamp(0);
+        if constexpr (N > 0) {
+            if (wave == helper) {
+                // prefetch the waiter lists of the task's promises (the CSR is
+                // static); wave 0 reads them after the task's barrier
+                uint32_t p[N];
+                Kind::promises(ctx, t, p);
+                uint32_t my_p = 0, b = 0, e = 0;
+#pragma unroll
+                for (int i = 0; i < N; ++i)
+                    if (lane == i) my_p = p[i];
+                if (lane < N) {
+                    b = view.waiter_off[my_p];
+                    e = view.waiter_off[my_p + 1];
+                }
+                uint32_t ub[N], un[N], upre[N], total = 0;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    ub[i] = (uint32_t)__builtin_amdgcn_readlane((int)b, i);
+                    un[i] = (uint32_t)__builtin_amdgcn_readlane((int)e, i) - ub[i];
+                    upre[i] = total;
+                    total += un[i];
+                }
+                if (total <= 64) {
+                    uint32_t idx = 0;
+#pragma unroll
+                    for (int i = 0; i < N; ++i)
+                        if ((uint32_t)lane >= upre[i] && (uint32_t)lane < upre[i] + un[i])
+                            idx = ub[i] + ((uint32_t)lane - upre[i]);
+                    if ((uint32_t)lane < total) sh.waiter[lane] = view.waiters[idx];
+                }
+                if (lane == 0) sh.nwait = total;
+            }
+        }
         const bool ok = Kind::run_group(ctx, t, view.payload + (size_t)t * view.payload_words, wave);
+        uint32_t was = 0;
+        if constexpr (N > 0) {
+            // the helper (usually the wave storing the task's last outputs)
+            // publishes the datums and marks the promises satisfied behind the
+            // same drain as its outputs
+            if (wave == helper && sh.nwait <= 64) {
+                uint32_t p[N];
+                unsigned long long d[N];
+                Kind::promises(ctx, t, p);
+                Kind::datums(ctx, t, d);
+                uint32_t my_p = 0;
+                unsigned long long my_d = 0;
+#pragma unroll
+                for (int i = 0; i < N; ++i)
+                    if (lane == i) {
+                        my_p = p[i];
+                        my_d = d[i];
+                    }
+                if (lane < N) {
+                    st_agent(&view.datum[my_p], my_d);
+                    was = __hip_atomic_exchange(&view.satisfied[my_p], 1u, __ATOMIC_RELAXED, HX_AGENT);
+                }
+            }
+        }
         vm_drain();
+        if constexpr (N > 0) {
+            if (wave == helper) {
+                const bool dbl = __ballot(lane < N && was != 0) != 0;  // src/hclib-promise.c:206-207
+                if (lane == 0) sh.dbl = dbl ? 1u : 0u;
+            }
+        }
         if (__syncthreads_or(!ok)) break;
         stamp(1);
-        if (wave == 0) {
-            Kind::put(ctx, w, t);
-            if (kept && lane == pend_lane) st_agent(&view.ready[pend_pos], kDagSkip);
+        if constexpr (N > 0) {
+            if (wave == 0) {
+                const uint32_t nwait = sh.nwait;
+                if (nwait > 64) {
+                    uint32_t p[N];
+                    unsigned long long d[N];
+                    Kind::promises(ctx, t, p);
+                    Kind::datums(ctx, t, d);
+                    // long waiter lists: the ordinary batched put (it appends
+                    // its releases itself)
+                    dag_put_n<N, Kind::kSc1Payload>(w, p, d);
+                    if (w.next != kDagEmpty && lane == w.skip_lane) st_agent(&view.ready[w.skip_pos], kDagSkip);
+                    if (lane == 0) {
+                        sh.npend = 0;
+                        sh.skip = 0;
+                    }
+                } else {
+                    const bool dbl = sh.dbl != 0;
+                    if (dbl && lane == 0) dev_error(view.err, kErrDoublePut);
+                    uint32_t rt = kDagEmpty;
+                    if (!dbl && (uint32_t)lane < nwait) {
+                        const uint32_t c = sh.waiter[lane];
+                        if (add_agent(&view.deps[c], (uint32_t)-1) == 1u) rt = c;
+                    }
+                    unsigned long long m = __ballot(rt != kDagEmpty);
+                    uint32_t skip = 0;
+                    if (m) {  // keep the first released task (see dag_put_one)
+                        const int leader = __builtin_ctzll(m);
+                        w.next = (uint32_t)__builtin_amdgcn_readlane((int)rt, leader);
+                        m &= m - 1;
+                        skip = 1;
+                    }
+                    // the others, compacted, for the helper wave's append
+                    if ((m >> lane) & 1ull) {
+                        const uint32_t r = (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        sh.pend[r] = rt;
+                    }
+                    if (lane == 0) {
+                        sh.npend = (uint32_t)__builtin_popcountll(m);
+                        sh.skip = skip;
+                    }
+                    w.puts += N;
+                    w.releases += (unsigned long long)(__builtin_popcountll(m) + skip);
+                }
+                // the kept task's ready slot is appended by the helper wave
+                w.skip_lane = 0;
+            }
+            __syncthreads();  // sh.pend / npend / skip before the helper reads them
+        } else {
+            if (wave == 0) {
+                Kind::put(ctx, w, t);
+                if (kept && lane == pend_lane) st_agent(&view.ready[pend_pos], kDagSkip);
+            }
         }
         stamp(2);
         ++ran;

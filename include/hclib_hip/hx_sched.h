@@ -133,6 +133,8 @@ struct SchedConfig {
                          // (no ring push / pop) while they fit one batch and no hungry
                          // wave could take them (see run_worker); 2 also runs narrow
                          // frontiers in a tight carry-to-carry loop, 1 does not
+    uint32_t hunger_fast = 0;  // batches between hunger reads while many waves are
+                               // hungry (0: (hunger + 3) / 4)
 };
 
 // Kind concept:
@@ -733,7 +735,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 // many hungry waves (ramp-up, a narrowing tree): read again
                 // soon; otherwise every cfg.hunger batches
                 const uint32_t hg = cfg.nwaves > outst_cur ? cfg.nwaves - outst_cur : 0u;
-                hunger_in = hg * 8u > cfg.nwaves ? (cfg.hunger + 3u) / 4u : cfg.hunger;
+                const uint32_t fast = cfg.hunger_fast ? cfg.hunger_fast : (cfg.hunger + 3u) / 4u;
+                hunger_in = hg * 8u > cfg.nwaves ? fast : cfg.hunger;
             }
             --hunger_in;
             outst = outst_cur;
