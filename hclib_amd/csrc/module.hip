@@ -38,9 +38,13 @@ int ensure_device() {
                                                                            : HCLIB_HIP_ENODEV;
 }
 
+// slot control pairs {seq, cnt}: slot i is free for ticket i (mod cap)
 __global__ void k_reset_pool(uint32_t *seq, uint32_t cap, uint32_t total) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < total) seq[i] = i & (cap - 1);
+    if (i < total) {
+        seq[2 * i] = i & (cap - 1);
+        seq[2 * i + 1] = 0;
+    }
 }
 
 int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolView *out) {
@@ -65,10 +69,10 @@ int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolVie
     char *p = (char *)m.pool_mem;
     out->hdr = (QueueHdr *)p;
     p += hdr;
+    // {seq, cnt} pairs, 8-B aligned (hx_sched.h slot_ctl); cnt = seq + 1
     out->seq = (uint32_t *)p;
-    p += slots * 4;
-    out->cnt = (uint32_t *)p;
-    p += slots * 4;
+    out->cnt = out->seq + 1;
+    p += slots * 8;
     p = (char *)(((uintptr_t)p + 255) & ~(uintptr_t)255);
     out->data = (uint32_t *)p;
     out->nq = nq;

@@ -631,6 +631,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     cfg.hunger_fast = (uint32_t)env_int("HCLIB_HIP_HUNGER_FAST", 0);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
     cfg.backoff = (uint32_t)env_int("HCLIB_HIP_BACKOFF", 16);
+    cfg.defer = (uint32_t)env_int("HCLIB_HIP_DEFER", 1);
     HX_TRY(reset_sched(pool, 1));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     const bool feat = nshards > 1 || max_levels > 0;

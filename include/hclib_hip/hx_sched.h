@@ -135,6 +135,8 @@ struct SchedConfig {
                          // frontiers in a tight carry-to-carry loop, 1 does not
     uint32_t hunger_fast = 0;  // batches between hunger reads while many waves are
                                // hungry (0: (hunger + 3) / 4)
+    uint32_t defer = 1;  // a hunger spill's chunk is published after the next batch body
+                         // (PendingChunk) instead of behind a store round trip
 };
 
 // Kind concept:
@@ -261,34 +263,73 @@ __device__ __forceinline__ void handoff_consume() {
 }
 __device__ __forceinline__ uint32_t lane0(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Try to publish `n` entries (ring positions bot..bot+n-1) as one chunk into
-// deque q. Called by the whole wave; returns true if published.
+// Chunk slot control word pair {seq, cnt} (8 B, one atomic 64-bit load reads
+// both): seq = pos when the slot is free for ticket pos, pos + 1 once that
+// ticket's chunk is published (cnt = its item count, stored before the
+// publish drain, so a load that sees the new seq sees the new cnt).
+__device__ __forceinline__ uint32_t *slot_ctl(const PoolView &pool, uint32_t slot) { return pool.seq + 2u * slot; }
+
+// A chunk whose payload is written but whose seq word is not yet stored: the
+// producer publishes it after its next batch's body, when the payload stores
+// have long landed (the drain is free there) instead of waiting a round trip
+// for them while it holds the rest of its items.
+struct PendingChunk {
+    uint32_t slot, pos, q;
+    bool live;
+};
+
 template <class Kind, int CAP>
-__device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
-                              WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n) {
+__device__ __forceinline__ void publish_pending(const PoolView &pool, SchedGlobals *g, PendingChunk &pc) {
+    if (!pc.live) return;
+    handoff_publish();  // the payload + cnt stores are complete
+    if (lane_id() == 0) {
+        st_agent(slot_ctl(pool, pc.slot), pc.pos + 1);
+        st_agent(&g->hint, pc.q);
+    }
+    pc.live = false;
+}
+
+// Try to publish `n` entries (ring positions bot..bot+n-1) as one chunk into
+// deque q. Called by the whole wave; returns true if the chunk is placed.
+// `occ`: the deque occupancy this wave saw at its last enqueue. While that
+// is low, the ticket is taken at once (one fetch-add, the head read beside
+// it refreshes `occ`); once it was high, the occupancy is read first and a
+// ring at least half full is refused, so a ticket never waits behind a
+// consumer that cannot come. With `pc`, the publish is deferred (see
+// PendingChunk); the caller must publish a live one before the next enqueue.
+template <class Kind, int CAP>
+__device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q, WaveStack<Kind, CAP> &st,
+                              uint32_t bot, uint32_t n, uint32_t &occ, PendingChunk *pc) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     QueueHdr *h = &pool.hdr[q];
-    uint32_t pos = 0;
+    uint32_t pos = 0, seen = 0;
     int ok = 0;
+    const bool fast = occ < pool.cap / 4;
     if (lane == 0) {
-        // a producer takes a ticket with ONE fetch-add (no CAS retry storms);
-        // it only does so while the ring is at most half full, so a ticket
-        // never waits behind a consumer that cannot come
-        const uint32_t hd = ld_agent(&h->head), tl = ld_agent(&h->tail);
-        if ((int)(tl - hd) < (int)(pool.cap / 2)) {
+        if (fast) {
             add_agent(&g->outstanding, 1u);  // counts before it becomes visible
             pos = add_agent(&h->tail, 1u);
+            seen = pos - ld_agent(&h->head);
             ok = 1;
+        } else {
+            const uint32_t hd = ld_agent(&h->head), tl = ld_agent(&h->tail);
+            seen = tl - hd;
+            if ((int)(tl - hd) < (int)(pool.cap / 2)) {
+                add_agent(&g->outstanding, 1u);
+                pos = add_agent(&h->tail, 1u);
+                ok = 1;
+            }
         }
     }
+    occ = lane0(seen);
     if (!lane0((uint32_t)ok)) return false;
     pos = lane0(pos);
     const uint32_t slot = q * pool.cap + (pos & (pool.cap - 1));
     if (lane == 0) {
         // the slot is free once its previous lap was consumed (normally at once)
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (ld_agent(&pool.seq[slot]) != pos) {
+        while (ld_agent(slot_ctl(pool, slot)) != pos) {
             if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s
                 dev_error(&g->err, kErrQueueFull);
                 break;
@@ -308,10 +349,17 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
 #pragma unroll
         for (int i = 0; i < W; ++i) st_agent(&dst[(uint32_t)lane * W + i], w[i]);
     }
-    if (lane == 0) st_agent(&pool.cnt[slot], n);
+    if (lane == 0) st_agent(slot_ctl(pool, slot) + 1, n);
+    if (pc) {
+        pc->slot = slot;
+        pc->pos = pos;
+        pc->q = q;
+        pc->live = true;
+        return true;
+    }
     handoff_publish();
     if (lane == 0) {
-        st_agent(&pool.seq[slot], pos + 1);
+        st_agent(slot_ctl(pool, slot), pos + 1);
         st_agent(&g->hint, q);
     }
     // nothing stays in flight past a spill (see vm_drain)
@@ -320,7 +368,9 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
 }
 
 // Try to take one chunk from deque q into the (empty) stack. Returns the
-// number of entries taken (0 if the deque looked empty).
+// number of entries taken (0 if the deque looked empty). Round trips: the
+// head/tail read, the head CAS, the {seq, cnt} pair, the payload; the slot
+// is handed back with a store nobody waits for.
 template <class Kind, int CAP>
 __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Kind, CAP> &st,
                                   SchedGlobals *g) {
@@ -340,10 +390,16 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
     if (!lane0((uint32_t)ok)) return 0;
     pos = lane0(pos);
     const uint32_t slot = q * pool.cap + (pos & (pool.cap - 1));
+    uint32_t cnt = 0;
     if (lane == 0) {
         // the producer holds this ticket and is publishing it (bounded wait)
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (ld_agent(&pool.seq[slot]) != pos + 1) {
+        while (true) {
+            const unsigned long long sc = ld_agent((const unsigned long long *)slot_ctl(pool, slot));
+            if ((uint32_t)sc == pos + 1) {
+                cnt = (uint32_t)(sc >> 32);
+                break;
+            }
             if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s
                 dev_error(&g->err, kErrSpinTimeout);
                 break;
@@ -354,7 +410,7 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
     handoff_consume();
     // uniform (readfirstlane): the ring bounds derived from it stay in SGPRs,
     // so every scheduler branch and loop of the batch is scalar
-    const uint32_t n = lane0(ld_agent(&pool.cnt[slot]));
+    const uint32_t n = lane0(cnt);
     // lane i unpacks item i: its own template slot (delta 0)
     const uint32_t *src = pool.data + (size_t)slot * pool.chunk * W;
     if ((uint32_t)lane < n) {
@@ -366,8 +422,7 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
     }
     // all reads of the slot have landed before it is handed back
     vm_drain();
-    if (lane == 0) st_agent(&pool.seq[slot], pos + pool.cap);
-    vm_drain();
+    if (lane == 0) st_agent(slot_ctl(pool, slot), pos + pool.cap);
     // one wave per workgroup: its LDS ops complete in issue order
     return n;
 }
@@ -609,6 +664,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     // next batch instead of round-tripping through the LDS ring
     uint32_t carry = 0, ck = 0;
     uint32_t ctmpl[TW];
+    PendingChunk pend;  // a spilled chunk waiting for its publish (see PendingChunk)
+    pend.live = false;
+    uint32_t occ = 0;   // deque occupancy seen at the last enqueue
 #pragma unroll
     for (int i = 0; i < TW; ++i) ctmpl[i] = 0;
 
@@ -650,6 +708,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         carry = lane0(carry);
         const uint32_t size = top - bot;
         if (size == 0 && carry == 0) {
+            publish_pending<Kind, CAP>(pool, g, pend);
             if (busy_phase) {
                 const unsigned long long now = __builtin_amdgcn_s_memtime();
                 cyc_busy += now - t_mark;
@@ -780,6 +839,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         } else {
             if (has) cnt = Kind::process(ctx, acc, tmpl, k, child, &g->err, true);
         }
+        // the previous batch's spilled chunk: its payload stores landed while
+        // this batch ran
+        publish_pending<Kind, CAP>(pool, g, pend);
         if (HX_STAMPS && cfg.stamps) {
             const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
             cyc_proc += ts1 - tsl;
@@ -871,7 +933,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             if (n > pool.chunk) n = pool.chunk;
             bool ok = false;
             for (uint32_t a = 0; a < pool.nq && !ok; ++a)
-                ok = enqueue_chunk<Kind, CAP>(pool, g, (home + a) % pool.nq, st, bot, n);
+                ok = enqueue_chunk<Kind, CAP>(pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr);
             if (!ok) {
                 // every deque is at its half-capacity mark: other waves are
                 // draining them, so wait (bounded) rather than fail at once
@@ -909,9 +971,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 if (n == 0 || n == sz) break;
                 // home deque first, then the other deques of this XCD slice
                 bool ok = false;
+                publish_pending<Kind, CAP>(pool, g, pend);  // one deferred chunk at a time
                 for (uint32_t a = 0; a < qpx && !ok; ++a) {
                     const uint32_t q = xcc * qpx + (home - xcc * qpx + a) % qpx;
-                    ok = enqueue_chunk<Kind, CAP>(pool, g, q, st, bot, n);
+                    ok = enqueue_chunk<Kind, CAP>(pool, g, q, st, bot, n, occ, cfg.defer ? &pend : nullptr);
                 }
                 if (!ok) break;  // deques full: keep the items (the ring still has room)
                 ++npush;
@@ -923,6 +986,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         }
         if (HX_STAMPS && cfg.stamps) t_batch = __builtin_amdgcn_s_memtime();
     }
+    publish_pending<Kind, CAP>(pool, g, pend);  // (error exits)
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
     const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
     if (busy_phase) cyc_busy += t_end - t_mark;
