@@ -169,12 +169,16 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
         int n = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) n += c.thr16[k] <= r ? 1 : 0;
-        if (n == 16) {  // rare: thresholds 17..100 of table 0 (device memory, L2-resident)
+        if (n == 16) {
+            // thresholds 17..100 of table 0, binary-searched in the LDS copy:
+            // P(n > 16) = 0.8^17 ~ 2.3% per node at b = 4, so ~3 of 4 batches
+            // of 64 have such a lane — a search through device memory (seven
+            // dependent L2 round trips) cost those batches more than their SHA-1
             int lo = 16, hi = 100;
             for (int s = 0; s < 7; ++s) {
                 int mid = (lo + hi + 1) >> 1;
                 if (lo < hi) {
-                    if (c.thr[mid] <= r) lo = mid;
+                    if (s_thr[mid] <= r) lo = mid;
                     else hi = mid - 1;
                 }
             }
@@ -303,6 +307,9 @@ __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, Sc
     constexpr int kUtsCap = CAP;
     __shared__ WaveStack<UtsKind<MODE, FEAT, CAP>, kUtsCap> st;
     if (MODE == kUtsGeoFixed) {
+        // table 0 in LDS for the rare tail search (uts_nc)
+        for (int i = threadIdx.x; i < 128; i += 64) s_thr[i] = ctx.thr[i];
+        __syncthreads();
         // the 16 thresholds compared per node live in VGPRs (wave-uniform
         // values the compiler would otherwise keep in SGPRs, spilling the
         // scheduler's scalar state around the batch loop)
@@ -606,11 +613,11 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     int wpc_default = 2, ring_default = 512;
     if (!bin) {
         const double est = (params->type == 1 && params->shape_fn == 3) ? pow(params->b_0, (double)params->gen_mx) : 1e9;
-        wpc_default = est >= 3e7 ? 8 : 4;
+        wpc_default = est >= 3e7 ? 8 : 2;
         // and a small tree runs faster on 256-item rings (one piece per task:
-        // the frontier fans out by range splitting) at 4 waves per CU: T1
-        // 0.98 -> 0.75 ms; a large one slower (T1XL 52 -> 70 ms),
-        // profiles/r02/sweep_t1_ring_waves.log, sweep_t1xl_ring_waves.log
+        // the frontier fans out by range splitting) at 2 waves per CU: T1
+        // 0.98 -> 0.70 ms; a large one slower (T1XL 52 -> 70 ms),
+        // profiles/r02/sweep_t1_ring_waves.log, sweep_t1xl_ring_waves.log, geo_lds_tail.log
         ring_default = est >= 3e7 ? 512 : 256;
     }
     const int grid = env_int("HCLIB_HIP_GRID", 0) > 0
