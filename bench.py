@@ -36,6 +36,8 @@ T1 = "-t 1 -a 3 -d 10 -b 4 -r 19"
 T1_GOLD = (4130071, 3305118, 10)          # test/uts/sample_trees.sh:17-18
 T1XL = "-t 1 -a 3 -d 15 -b 4 -r 29"
 T1XL_GOLD = (1635119272, 1308100063, 15)  # test/uts/sample_trees.sh:50-51
+T1L = "-t 1 -a 3 -d 13 -b 4 -r 29"
+T1L_GOLD = (102181082, 81746377, 13)      # test/uts/sample_trees.sh:36-37
 HBM_PEAK_GBS = 8000.0                      # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -81,6 +83,55 @@ def wide_tree(H, rank, world, be, steps=2, split=7):
         one = dist.max_over_ranks(time.perf_counter() - t1, world, be)
         out["ms_one_gpu"] = one * 1e3
         out["efficiency"] = one / (world * el / steps)
+    return out
+
+
+def skewed_sharing(H, rank, world, be, split=1):
+    """Cross-GPU work sharing (dist.GlobalPool) on a
+    partition the static hash cannot balance: T1L split at depth 1 (a handful
+    of depth-1 subtrees over `world` shards). Searched once with the static
+    partition only and once sharing work through the region in rank 0's HBM;
+    bit-exact both ways. Any failure is reported in the line, not raised."""
+    from hclib_amd import dist
+
+    out = {"workload": f"test/uts T1L ({T1L}) sharded over {world} GPU(s), split depth {split}: "
+                       "static partition vs cross-GPU work sharing"}
+    pool, err = None, ""
+    try:
+        pool = dist.GlobalPool(rank, world, be)
+    except Exception as e:  # noqa: BLE001 (reported, every rank reaches the collective below)
+        err = f"setup: {e}"
+    if dist.max_over_ranks(1.0 if pool is None else 0.0, world, be) != 0.0:
+        out["error"] = err or "setup failed on another rank"
+        return out
+    for shared in (False, True):
+        if shared:
+            H.global_attach(pool.ptr, pool.cap, rank)
+            pool.reset()
+        else:
+            H.global_attach(None)
+            dist.barrier(world, be)
+        t0 = time.perf_counter()
+        r = None
+        try:
+            r = H.uts(T1L, rank, world, split)
+        except Exception as e:  # noqa: BLE001
+            err = str(e)
+        el = dist.max_over_ranks(time.perf_counter() - t0, world, be)
+        if dist.max_over_ranks(1.0 if r is None else 0.0, world, be) != 0.0:
+            out["error"] = err or "search failed on another rank"
+            break
+        tot = dist.combine_counts(r["nodes"], r["leaves"], r["max_depth"], world, be)
+        key = "shared" if shared else "static"
+        out[key] = {"ms": el * 1e3, "bit_exact": tot == T1L_GOLD,
+                    "nodes_per_rank": [int(n) for n in dist.gather_floats(float(r["nodes"]), world, be)],
+                    "kernel_ms_per_rank": dist.gather_floats(r["kernel_ms"], world, be)}
+    if "error" not in out:
+        g = pool.read()
+        out["shared"].update({"chunks_exported": g["exported"][:world], "chunks_imported": g["imported"][:world]})
+        out["speedup"] = out["static"]["ms"] / out["shared"]["ms"]
+    H.global_attach(None)
+    pool.close()
     return out
 
 
@@ -352,6 +403,9 @@ def main():
     shard_sw = None
     if world > 1 and not args.no_extras:
         shard_sw = sharded_sw(H, rank, world, be)
+    skewed = None
+    if world > 1 and not args.no_extras and os.environ.get("HCLIB_BENCH_SHARE_WORK", "1") != "0":
+        skewed = skewed_sharing(H, rank, world, be)
     if rank != 0:
         dist.shutdown(world)
         return
@@ -391,6 +445,8 @@ def main():
         out["forasync_sharded"] = shard_tri
     if shard_sw:
         out["sw_sharded"] = shard_sw
+    if skewed:
+        out["uts_work_sharing"] = skewed
     if world == 1 and not args.no_extras:
         tri = measure_triad(H)
         traffic = load_pmc_traffic()

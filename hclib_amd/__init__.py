@@ -119,6 +119,14 @@ def lib():
                                             C.POINTER(C.c_uint64)]
         L.hclib_hip_atomic_calibrate.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double),
                                                  C.POINTER(C.c_double)]
+        L.hclib_hip_global_bytes.restype = C.c_size_t
+        L.hclib_hip_global_bytes.argtypes = [C.c_uint32]
+        L.hclib_hip_global_init.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
+        L.hclib_hip_global_attach.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
+        L.hclib_hip_global_read.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        L.hclib_hip_ipc_export.argtypes = [C.c_void_p, C.c_void_p]
+        L.hclib_hip_ipc_import.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+        L.hclib_hip_ipc_close.argtypes = [C.c_void_p]
         _lib = L
     return _lib
 
@@ -207,6 +215,45 @@ def uts_num_children_host(params, height: int, state_words) -> int:
 
 
 # ----------------------------------------------------------------------- fib
+def global_bytes(cap: int) -> int:
+    """Bytes of a cross-GPU work-sharing region with `cap` chunk slots."""
+    n = lib().hclib_hip_global_bytes(cap)
+    if n == 0:
+        raise HclibError("global_bytes: cap must be a power of two >= 2")
+    return n
+
+
+def global_init(region: int, cap: int, nranks: int) -> None:
+    _check(lib().hclib_hip_global_init(region, cap, nranks), "hclib_hip_global_init")
+
+
+def global_attach(region: Optional[int], cap: int = 0, rank: int = 0) -> None:
+    _check(lib().hclib_hip_global_attach(region, cap, rank), "hclib_hip_global_attach")
+
+
+def global_read(region: int) -> dict:
+    out = (C.c_uint64 * 35)()
+    _check(lib().hclib_hip_global_read(region, out), "hclib_hip_global_read")
+    return {"active": out[0], "idle": out[1], "queued": out[2],
+            "exported": [out[3 + 2 * r] for r in range(16)], "imported": [out[4 + 2 * r] for r in range(16)]}
+
+
+def ipc_export(dev_ptr: int) -> bytes:
+    h = (C.c_char * 64)()
+    _check(lib().hclib_hip_ipc_export(dev_ptr, h), "hclib_hip_ipc_export")
+    return bytes(h)
+
+
+def ipc_import(handle: bytes) -> int:
+    p = C.c_void_p()
+    _check(lib().hclib_hip_ipc_import(C.c_char_p(handle), C.byref(p)), "hclib_hip_ipc_import")
+    return p.value
+
+
+def ipc_close(dev_ptr: int) -> None:
+    _check(lib().hclib_hip_ipc_close(dev_ptr), "hclib_hip_ipc_close")
+
+
 def fib(n: int):
     v = C.c_int64()
     r = FibResult()

@@ -31,6 +31,9 @@ struct Module {
     WaveStat *wave_stats = nullptr;
     uint32_t wave_stats_cap = 0;
     std::vector<WaveStat> last_waves;  // the last launch's, copied back by finish_sched
+    // cross-GPU work sharing (hclib_hip_global_attach): the shared region's
+    // view for sharded launches, hdr null while detached
+    GlobalView gview = {nullptr, nullptr, nullptr, 0, 0};
 };
 
 Module &mod();
@@ -44,7 +47,7 @@ int upload_async(void *dst, const void *src, size_t bytes, hipStream_t stream);
 // Carve a PoolView for `words` u32 per entry out of the arena (grows it).
 int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolView *out);
 // Reset the deques and the globals on the module stream before a launch.
-int reset_sched(const PoolView &pool, uint32_t outstanding_init);
+int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global = false);
 // Read back globals and translate the device error word.
 int finish_sched(SchedGlobals *host_copy, const char *who);
 

@@ -132,7 +132,7 @@ int upload_async(void *dst, const void *src, size_t bytes, hipStream_t st) {
     return HCLIB_HIP_OK;
 }
 
-int reset_sched(const PoolView &pool, uint32_t outstanding_init) {
+int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global) {
     Module &m = g_mod;
     HX_HIP(hipMemsetAsync(pool.hdr, 0, sizeof(QueueHdr) * pool.nq, m.stream));
     const uint32_t total = pool.nq * pool.cap;
@@ -144,6 +144,7 @@ int reset_sched(const PoolView &pool, uint32_t outstanding_init) {
     init.outstanding = outstanding_init;
     init.wave_stats = m.wave_stats;
     init.wave_stats_cap = m.wave_stats_cap;
+    if (global) init.gview = m.gview;
     // a pinned staging copy of its own, reused: every launch ends with the
     // stream synchronised (hclib_hip_sched_end), so the last copy is done
     static SchedGlobals *stage = nullptr;
@@ -310,3 +311,117 @@ int hclib_hip_num_workers(void) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------- cross-GPU work sharing
+// One region (GlobalHdr + cap {seq, cnt} pairs + cap chunk payloads) in one
+// rank's HBM, mapped into every other rank's process over IPC
+// (hclib_hip_ipc_export / _import); every sharded UTS launch of a rank that
+// attached it shares work through it (hx_sched.h GlobalView).
+static size_t global_layout(uint32_t cap, size_t *ctl_off, size_t *data_off) {
+    const size_t words = 64 * 8;  // a chunk: up to 64 entries of 8 words (UTS, fib)
+    const size_t hdr = (sizeof(GlobalHdr) + 255) & ~(size_t)255;
+    const size_t ctl = ((size_t)cap * 8 + 255) & ~(size_t)255;
+    *ctl_off = hdr;
+    *data_off = hdr + ctl;
+    return hdr + ctl + (size_t)cap * words * 4;
+}
+
+extern "C" size_t hclib_hip_global_bytes(uint32_t cap) {
+    size_t a, b;
+    if (cap < 2 || (cap & (cap - 1))) return 0;
+    return global_layout(cap, &a, &b);
+}
+
+__global__ void k_reset_global(uint32_t *ctl, uint32_t cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cap) {
+        ctl[2 * i] = i;
+        ctl[2 * i + 1] = 0;
+    }
+}
+
+extern "C" int hclib_hip_global_init(void *region, uint32_t cap, int nranks) {
+    if (!region || cap < 2 || (cap & (cap - 1)) || nranks < 1 || nranks > kGlobalMaxRanks) {
+        set_error("hclib_hip_global_init: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    Module &m = g_mod;
+    size_t co, dof;
+    global_layout(cap, &co, &dof);
+    HX_HIP(hipMemsetAsync(region, 0, co, m.stream));
+    hipLaunchKernelGGL(k_reset_global, dim3((cap + 255) / 256), dim3(256), 0, m.stream,
+                       (uint32_t *)((char *)region + co), cap);
+    HX_HIP(hipGetLastError());
+    // every rank starts holding its shard's top levels
+    const uint32_t active = (uint32_t)nranks;
+    HX_HIP(hipMemcpyAsync(region, &active, 4, hipMemcpyHostToDevice, m.stream));
+    HX_HIP(hipStreamSynchronize(m.stream));
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_global_attach(void *region, uint32_t cap, int rank) {
+    HX_TRY(ensure_device());
+    Module &m = g_mod;
+    if (!region) {
+        m.gview = GlobalView{nullptr, nullptr, nullptr, 0, 0};
+        return HCLIB_HIP_OK;
+    }
+    if (cap < 2 || (cap & (cap - 1)) || rank < 0 || rank >= kGlobalMaxRanks) {
+        set_error("hclib_hip_global_attach: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    size_t co, dof;
+    global_layout(cap, &co, &dof);
+    m.gview.hdr = (GlobalHdr *)region;
+    m.gview.ctl = (uint32_t *)((char *)region + co);
+    m.gview.data = (uint32_t *)((char *)region + dof);
+    m.gview.cap = cap;
+    m.gview.rank = (uint32_t)rank;
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_global_read(const void *region, uint64_t out[3 + 2 * kGlobalMaxRanks]) {
+    if (!region || !out) {
+        set_error("hclib_hip_global_read: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    GlobalHdr h;
+    HX_HIP(hipMemcpy(&h, region, sizeof(h), hipMemcpyDeviceToHost));
+    out[0] = h.active;
+    out[1] = h.idle;
+    out[2] = h.tail - h.head;
+    for (int i = 0; i < 2 * kGlobalMaxRanks; ++i) out[3 + i] = h.moved[i];
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_ipc_export(void *dev_ptr, void *handle_out) {
+    if (!dev_ptr || !handle_out) {
+        set_error("hclib_hip_ipc_export: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    hipIpcMemHandle_t h;
+    HX_HIP(hipIpcGetMemHandle(&h, dev_ptr));
+    memcpy(handle_out, &h, sizeof(h));
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_ipc_import(const void *handle, void **dev_ptr_out) {
+    if (!handle || !dev_ptr_out) {
+        set_error("hclib_hip_ipc_import: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    HX_HIP(hipIpcOpenMemHandle(dev_ptr_out, h, hipIpcMemLazyEnablePeerAccess));
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_ipc_close(void *dev_ptr) {
+    HX_TRY(ensure_device());
+    HX_HIP(hipIpcCloseMemHandle(dev_ptr));
+    return HCLIB_HIP_OK;
+}

@@ -250,6 +250,13 @@ struct UtsKind {
         }
     };
 
+    // cross-GPU sharing (GLOBAL launches): a task may move to another rank
+    // once its children lie below the shard split (the levels above it are
+    // expanded by every rank and counted by shard 0)
+    __device__ static bool movable(const Ctx &c, const uint32_t *tmpl) {
+        return c.nshards <= 1 || (int)tmpl[5] >= c.split;
+    }
+
     __device__ static int roots(const Ctx &c, Acc &acc, uint32_t *tmpl) {
         // the root node (height 0) is counted once, by shard 0
         if (lane_id() == 0 && c.shard == 0) {
@@ -301,7 +308,9 @@ struct UtsKind {
     }
 };
 
-template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512)>
+// GLOBAL: a sharded launch that shares work with the other ranks
+// (hclib_hip_global_attach; hx_sched.h GlobalView)
+template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512), bool GLOBAL = false>
 __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, SchedGlobals *g,
                                                    SchedConfig cfg) {
     constexpr int kUtsCap = CAP;
@@ -316,7 +325,7 @@ __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, Sc
         UtsCtx lc = ctx;
 #pragma unroll
         for (int k = 0; k < 16; ++k) asm volatile("v_mov_b32 %0, %1" : "=v"(lc.thr16[k]) : "s"(ctx.thr16[k]));
-        run_worker<UtsKind<MODE, FEAT, CAP>, kUtsCap>(lc, pool, g, cfg, st, blockIdx.x == 0);
+        run_worker<UtsKind<MODE, FEAT, CAP>, kUtsCap, GLOBAL>(lc, pool, g, cfg, st, blockIdx.x == 0);
         return;
     }
     if (MODE == kUtsRulesLds) {
@@ -325,7 +334,7 @@ __global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, Sc
         for (int i = threadIdx.x; i < ctx.nthr; i += 64) s_thr[i] = ctx.thr[i];
         __syncthreads();
     }
-    run_worker<UtsKind<MODE, FEAT, CAP>, kUtsCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
+    run_worker<UtsKind<MODE, FEAT, CAP>, kUtsCap, GLOBAL>(ctx, pool, g, cfg, st, blockIdx.x == 0);
 }
 
 // ------------------------------------------------------ host: rules/tables
@@ -639,7 +648,9 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
     cfg.backoff = (uint32_t)env_int("HCLIB_HIP_BACKOFF", 16);
     cfg.defer = (uint32_t)env_int("HCLIB_HIP_DEFER", 1);
-    HX_TRY(reset_sched(pool, 1));
+    // sharded launches of a rank attached to a global region share work
+    const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
+    HX_TRY(reset_sched(pool, 1, global));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     const bool feat = nshards > 1 || max_levels > 0;
     if (bin) ctx.bin_thr = (uint32_t)T.rules[1].y;
@@ -659,6 +670,12 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
             return HCLIB_HIP_EINVAL;
         }
         kern = k_uts_search<kUtsBin, 2>;
+    }
+    if (global) {
+        static const uts_kernel_t gkernels[4] = {
+            k_uts_search<kUtsRulesGlobal, 1, 512, true>, k_uts_search<kUtsRulesLds, 1, 512, true>,
+            k_uts_search<kUtsBin, 1, 1024, true>, k_uts_search<kUtsGeoFixed, 1, 512, true>};
+        kern = gkernels[mode];
     }
     if (mode == kUtsGeoFixed && !feat) {  // ring-size variants of the fixed-shape GEO search
         const int ring = env_int("HCLIB_HIP_UTS_RING", ring_default);

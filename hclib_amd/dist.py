@@ -253,3 +253,69 @@ class ShardedSw:
         tt = torch.tensor([tiles], dtype=torch.int64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.SUM, group=self.group)
         return int(sc[0]), int(tt[0])
+
+
+class GlobalPool:
+    """Cross-GPU work sharing for sharded UTS searches:
+    one region in rank 0's HBM (hclib_hip_global_*), mapped into every other
+    rank's process over IPC; a rank's sharded searches then take chunks from
+    / export chunks to it, and every rank's launch ends when no rank holds
+    work. Collective: every rank constructs it, calls reset() before each
+    sharded search (rank 0 re-initialises the region between two barriers)
+    and close() at the end. `group` carries the handle and the barriers
+    (default: the world group)."""
+
+    def __init__(self, rank: int, world: int, backend: str = "nccl", cap: int = 1024, group=None):
+        import torch
+        import torch.distributed as dist
+
+        import hclib_amd as H
+
+        self.rank, self.world, self.cap, self.group = rank, world, cap, group
+        self.backend = backend
+        self._buf = None
+        self._imported = None
+        if rank == 0:
+            self._buf = torch.empty(H.global_bytes(cap), dtype=torch.uint8, device="cuda")
+            self.ptr = self._buf.data_ptr()
+            handle = [H.ipc_export(self.ptr)]
+        else:
+            handle = [None]
+        if world > 1:
+            dist.broadcast_object_list(handle, src=0, group=group)
+        if rank != 0:
+            self._imported = H.ipc_import(handle[0])
+            self.ptr = self._imported
+        H.global_attach(self.ptr, cap, rank)
+
+    def _barrier(self):
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier(group=self.group)
+
+    def reset(self):
+        import hclib_amd as H
+
+        self._barrier()
+        if self.rank == 0:
+            H.global_init(self.ptr, self.cap, self.world)
+        self._barrier()
+
+    def read(self) -> dict:
+        import hclib_amd as H
+
+        return H.global_read(self.ptr)
+
+    def close(self):
+        import hclib_amd as H
+
+        H.global_attach(None)
+        self._barrier()
+        if self._imported is not None:
+            H.ipc_close(self._imported)
+            self._imported = None
+        self._barrier()
+        self._buf = None

@@ -240,16 +240,40 @@ typedef struct {
 
 /* Search the whole tree on the bound GPU (persistent megakernel: per-wave
  * LDS stacks, per-XCD chunk deques in HBM, device-atomic stealing,
- * outstanding-work termination). Multi-GPU sharding: with nshards > 1 the
- * top of the tree is expanded identically on every shard until the
- * frontier holds >= min_frontier nodes; shard `shard` then searches the
- * frontier nodes whose index is congruent to shard (mod nshards) and counts
- * the expanded top nodes only when shard == 0. Per-shard results sum to
- * the whole tree (max for depth). level_hist (host, may be NULL) receives
- * nodes per depth for depth < max_levels (max_levels <= 1024). */
+ * outstanding-work termination). Multi-GPU sharding: with nshards > 1 every
+ * shard expands the levels above split_depth identically (counted by shard
+ * 0 only); shard `shard` keeps the depth-split_depth nodes whose first state
+ * word is congruent to shard (mod nshards) and searches their subtrees.
+ * Per-shard results sum to the whole tree (max for depth); with a global
+ * region attached (hclib_hip_global_*) subtrees below the split also move
+ * between shards. level_hist (host, may be NULL) receives nodes per depth
+ * for depth < max_levels (max_levels <= 65536). */
 int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int shard, int nshards,
-                         int min_frontier, hclib_hip_uts_result_t *result, uint64_t *level_hist,
+                         int split_depth, hclib_hip_uts_result_t *result, uint64_t *level_hist,
                          int max_levels);
+
+/* Cross-GPU work sharing for sharded searches (one process per GPU;
+ * SURVEY 8e items 2-3; the reference's distributed UTS moves work between
+ * ranks, test/performance-regression/full-apps/uts/uts_hclib_shmem_opt.cpp
+ * :98-140). One region of hclib_hip_global_bytes(cap) bytes lives in one
+ * rank's device memory; the other ranks map it with hclib_hip_ipc_import
+ * (handle from hclib_hip_ipc_export: HIP_IPC_HANDLE_SIZE = 64 bytes). Before
+ * each sharded launch one rank resets it (hclib_hip_global_init, nranks =
+ * ranks that will launch) and every rank waits for that (a barrier); a rank
+ * that attached it (hclib_hip_global_attach, NULL detaches) then shares
+ * work in every sharded hclib_hip_uts_search: idle waves take chunks from
+ * the region's ring, busy waves export chunks while some rank is idle, and
+ * each rank's launch ends only when no rank holds work (the region's
+ * `active` count, system-scope atomics). hclib_hip_global_read fills
+ * out[0] active, out[1] idle ranks, out[2] chunks queued, then per rank r
+ * out[3 + 2r] chunks exported and out[4 + 2r] chunks imported (r < 16). */
+size_t hclib_hip_global_bytes(uint32_t cap);
+int hclib_hip_global_init(void *region, uint32_t cap, int nranks);
+int hclib_hip_global_attach(void *region, uint32_t cap, int rank);
+int hclib_hip_global_read(const void *region, uint64_t out[35]);
+int hclib_hip_ipc_export(void *dev_ptr, void *handle_out);
+int hclib_hip_ipc_import(const void *handle, void **dev_ptr_out);
+int hclib_hip_ipc_close(void *dev_ptr);
 
 /* Host-side helper (no GPU needed): evaluate the integer numChildren rule
  * the device uses (threshold tables built from the reference's libm

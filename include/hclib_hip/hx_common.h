@@ -52,6 +52,27 @@ __device__ __forceinline__ bool cas_agent(T *p, T expected, T desired) {
                                                 __ATOMIC_RELAXED, HX_AGENT);
 }
 
+// system-scope forms: words shared with other GPUs (cross-GPU work sharing,
+// hx_sched.h GlobalView) — coherent across devices, not only across the XCDs
+// of one
+template <typename T>
+__device__ __forceinline__ T ld_sys(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ void st_sys(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ T add_sys(T *p, T v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ bool cas_sys(T *p, T expected, T desired) {
+    return __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // s_waitcnt vmcnt(0) the compiler's waitcnt pass can see (an inline-asm wait
 // is opaque to it: stores it still believes in flight make it insert a
 // vmcnt(0) before the next write to their data VGPRs — which also waits for

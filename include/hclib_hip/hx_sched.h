@@ -72,6 +72,40 @@ struct WaveStat {
 };
 static_assert(sizeof(WaveStat) == 128, "WaveStat is 16 words");
 
+// Cross-GPU work sharing (one process per GPU; SURVEY §8e items 2-3, the
+// reference's distributed UTS moves work between ranks, test/performance-
+// regression/full-apps/uts/uts_hclib_shmem_opt.cpp:98-140). One region in one
+// rank's HBM, mapped by every rank (IPC), every word system-scope:
+//   active  = ranks holding work + chunks queued in the global ring; the
+//             launch of EVERY rank ends when it reads 0 (the termination
+//             count the reference's ranks reach by messages)
+//   idle    = ranks with no local work: the global hunger signal
+//   a bounded MPMC ring of chunks (the local deques' slot format).
+// A rank counts as holding work while its local `outstanding` is non-zero:
+// the wave that takes it to 0 releases the rank's unit of `active`, a wave
+// that takes it from 0 (only a global steal can) re-acquires it before it
+// gives back the stolen chunk's unit, so `active` never reads 0 early.
+struct alignas(256) GlobalHdr {
+    uint32_t active;
+    uint32_t pad0[63];
+    uint32_t idle;
+    uint32_t pad1[63];
+    uint32_t head;
+    uint32_t pad2[63];
+    uint32_t tail;
+    uint32_t pad3[63];
+    unsigned long long moved[32];  // [2r] chunks rank r exported, [2r+1] chunks it imported
+};
+constexpr int kGlobalMaxRanks = 16;
+
+struct GlobalView {
+    GlobalHdr *hdr;  // null: this launch shares nothing
+    uint32_t *ctl;   // cap {seq, cnt} pairs (slot_ctl layout)
+    uint32_t *data;  // cap * chunk * words
+    uint32_t cap;    // slots (power of two)
+    uint32_t rank;
+};
+
 // Global scheduler state shared by all waves of one launch (device memory).
 struct alignas(256) SchedGlobals {
     uint32_t outstanding;  // chunks queued + waves holding work
@@ -85,6 +119,7 @@ struct alignas(256) SchedGlobals {
     WaveStat *wave_stats;             // per-wave records (indexed by blockIdx.x), or null
     uint32_t wave_stats_cap;          // records available
     unsigned long long narrow[4];     // narrow-frontier loop: [0] batches, [1] s_memtime cycles, [2] entries
+    GlobalView gview;                 // cross-GPU work sharing (gview.hdr null: off)
 };
 
 // Diagnostic build (-DHX_STAMPS=1): per-phase s_memtime stamps, enabled at run
@@ -427,6 +462,126 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
     return n;
 }
 
+// Export `n` entries (ring positions bot..) as one chunk into the global
+// ring (whole wave; false if the ring is half full). The chunk's unit of
+// `active` is taken before it becomes visible.
+// Only items the Kind calls movable leave the rank (UTS: nodes below the
+// shard split depth; the replicated top levels stay where they are counted).
+template <class Kind, int CAP>
+__device__ bool global_enqueue(const typename Kind::Ctx &ctx, const GlobalView &gv, uint32_t words_per_chunk,
+                               WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n, uint32_t *err) {
+    constexpr int W = Kind::kWords;
+    const int lane = lane_id();
+    GlobalHdr *h = gv.hdr;
+    // lane i packs item bot+i as {template, k, kend} (n <= 64)
+    uint32_t w[W];
+    bool mv = true;
+    if ((uint32_t)lane < n) {
+        const uint32_t p = bot + (uint32_t)lane;
+        const uint2 dd = st.d[p & (CAP - 1)];
+        load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & (CAP - 1), w);
+        w[W - 2] = dd.x;
+        w[W - 1] = dd.y & (kMaxChildren - 1);
+        mv = Kind::movable(ctx, w);
+    }
+    if (__ballot(!mv) != 0) return false;
+    uint32_t pos = 0;
+    int ok = 0;
+    if (lane == 0) {
+        const uint32_t hd = ld_sys(&h->head), tl = ld_sys(&h->tail);
+        if ((int)(tl - hd) < (int)(gv.cap / 2)) {
+            add_sys(&h->active, 1u);
+            pos = add_sys(&h->tail, 1u);
+            ok = 1;
+        }
+    }
+    if (!lane0((uint32_t)ok)) return false;
+    pos = lane0(pos);
+    const uint32_t slot = pos & (gv.cap - 1);
+    uint32_t *ctl = gv.ctl + 2u * slot;
+    if (lane == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (ld_sys(ctl) != pos) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s
+                dev_error(err, kErrQueueFull);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    uint32_t *dst = gv.data + (size_t)slot * words_per_chunk;
+    if ((uint32_t)lane < n) {
+#pragma unroll
+        for (int i = 0; i < W; ++i) st_sys(&dst[(uint32_t)lane * W + i], w[i]);
+    }
+    if (lane == 0) st_sys(ctl + 1, n);
+    vm_drain();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: visible to the other GPUs
+    if (lane == 0) {
+        st_sys(ctl, pos + 1);
+        if (gv.rank < (uint32_t)kGlobalMaxRanks) add_sys(&h->moved[2 * gv.rank], 1ull);
+    }
+    vm_drain();
+    return true;
+}
+
+// Take one chunk from the global ring into the (empty) stack; returns the
+// entries taken (0: none). The caller converts the chunk's unit of `active`
+// into its rank's (see GlobalHdr).
+template <class Kind, int CAP>
+__device__ uint32_t global_dequeue(const GlobalView &gv, uint32_t words_per_chunk, WaveStack<Kind, CAP> &st,
+                                   uint32_t *err) {
+    constexpr int W = Kind::kWords;
+    const int lane = lane_id();
+    GlobalHdr *h = gv.hdr;
+    uint32_t pos = 0;
+    int ok = 0;
+    if (lane == 0) {
+        const uint32_t hd = ld_sys(&h->head), tl = ld_sys(&h->tail);
+        if ((int)(tl - hd) > 0 && cas_sys(&h->head, hd, hd + 1)) {
+            pos = hd;
+            ok = 1;
+        }
+    }
+    if (!lane0((uint32_t)ok)) return 0;
+    pos = lane0(pos);
+    const uint32_t slot = pos & (gv.cap - 1);
+    uint32_t *ctl = gv.ctl + 2u * slot;
+    uint32_t cnt = 0;
+    if (lane == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (true) {
+            const unsigned long long sc = ld_sys((const unsigned long long *)ctl);
+            if ((uint32_t)sc == pos + 1) {
+                cnt = (uint32_t)(sc >> 32);
+                break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s
+                dev_error(err, kErrSpinTimeout);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint32_t n = lane0(cnt);
+    const uint32_t *src = gv.data + (size_t)slot * words_per_chunk;
+    if ((uint32_t)lane < n) {
+        uint32_t w[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) w[i] = ld_sys(&src[(uint32_t)lane * W + i]);
+        store_tmpl<Kind, CAP>(st, (uint32_t)lane, w);
+        st.d[lane] = make_uint2(w[W - 2], w[W - 1]);
+    }
+    vm_drain();
+    if (lane == 0) {
+        st_sys(ctl, pos + gv.cap);
+        if (gv.rank < (uint32_t)kGlobalMaxRanks) add_sys(&h->moved[2 * gv.rank + 1], 1ull);
+    }
+    vm_drain();
+    return n;
+}
+
 __device__ __forceinline__ uint32_t xorshift(uint32_t &s) {
     s ^= s << 13;
     s ^= s >> 17;
@@ -628,7 +783,27 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
     return ns;
 }
 
-template <class Kind, int CAP>
+// a wave stops holding work: local `outstanding` -1; the wave that takes it
+// to 0 releases its rank's unit of the global `active` (GLOBAL launches)
+template <bool GLOBAL>
+__device__ __forceinline__ void wave_goes_idle(SchedGlobals *g, const GlobalView &gv) {
+    if (lane_id() != 0) return;
+    if constexpr (GLOBAL) {
+        const uint32_t prev = __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+        if (prev == 1u) {
+            add_sys(&gv.hdr->idle, 1u);
+            add_sys(&gv.hdr->active, (uint32_t)-1);
+        }
+    } else {
+        __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+    }
+}
+
+// GLOBAL: the launch shares work with the other ranks through g->gview
+// (idle waves take chunks from the global ring, a wave holding spill_lo+
+// items exports a chunk while some rank is idle and none of its own waves
+// is hungry; termination waits for the global `active` count)
+template <class Kind, int CAP, bool GLOBAL = false>
 __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, SchedGlobals *g,
                            const SchedConfig &cfg, WaveStack<Kind, CAP> &st, bool seed_roots) {
     constexpr int TW = Kind::kTmplWords;
@@ -641,6 +816,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     static_assert(CAP >= kWaveSize * kGroupMax + kGroupMax, "ring must hold one batch's pushes");
     const int lane = lane_id();
     const uint32_t gid = blockIdx.x;
+    GlobalView gv;
+    if constexpr (GLOBAL) gv = g->gview;
+    uint32_t gidle_pf = 0, gidle = 0;  // GLOBAL: idle ranks, read with the hunger signal
     const uint32_t qpx = pool.nq / 8;
     const uint32_t xcc = xcc_id() & 7u;
     const uint32_t home = xcc * qpx + (gid / 8) % qpx;
@@ -686,7 +864,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         active = true;  // the host initialised outstanding = 1 for this wave
         if (top == 0) {
             active = false;
-            if (lane == 0) __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+            wave_goes_idle<GLOBAL>(g, gv);
         }
     }
 
@@ -717,8 +895,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             }
             if (active) {
                 active = false;
-                if (lane == 0)
-                    __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+                wave_goes_idle<GLOBAL>(g, gv);
             }
             // probe order: home, hint, then random (3/4 same XCD, 1/4 anywhere)
             uint32_t q = home;
@@ -732,6 +909,23 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 q = ((r & 3) != 0) ? xcc * qpx + (r >> 2) % qpx : (r >> 2) % pool.nq;
             }
             uint32_t n = dequeue_chunk<Kind, CAP>(pool, q, st, g);
+            if constexpr (GLOBAL) {
+                // every 4th probe that found nothing local: the global ring
+                if (n == 0 && (spins & 3) == 3) {
+                    n = global_dequeue<Kind, CAP>(gv, pool.chunk * (uint32_t)Kind::kWords, st, &g->err);
+                    if (n && lane == 0) {
+                        // this wave now holds work; a rank that had none takes
+                        // its unit of `active` back before the chunk's is returned
+                        const uint32_t prev = add_agent(&g->outstanding, 1u);
+                        if (prev == 0u) {
+                            add_sys(&gv.hdr->active, 1u);
+                            add_sys(&gv.hdr->idle, (uint32_t)-1);
+                        }
+                        add_sys(&gv.hdr->active, (uint32_t)-1);
+                    }
+                    if (n) q = home;  // (not counted as a local steal)
+                }
+            }
             if (n) {
                 if (q != home) {
                     ++nsteal;
@@ -759,7 +953,17 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     e = ld_agent(&g->err);
                 }
                 vm_drain();  // both loads land on every path (no phantom waits in the batch loop)
-                if (lane0(outst) == 0 || lane0(e)) break;
+                if (lane0(e)) break;
+                if (lane0(outst) == 0) {
+                    if constexpr (!GLOBAL) break;
+                    else {
+                        // no local work: the launch ends when no rank holds any
+                        uint32_t ga = 0;
+                        if (lane == 0) ga = ld_sys(&gv.hdr->active);
+                        vm_drain();
+                        if (lane0(ga) == 0) break;
+                    }
+                }
                 outst_pf = outst;  // fresh hunger signal for the first batch after a steal
                 hunger_in = 0;
             }
@@ -791,6 +995,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             if (hunger_in == 0) {
                 outst_cur = lane0(outst_pf);
                 if (lane == 0) outst_pf = ld_agent(&g->outstanding);
+                if constexpr (GLOBAL) {
+                    gidle = lane0(gidle_pf);
+                    if (lane == 0) gidle_pf = ld_sys(&gv.hdr->idle);
+                }
                 // many hungry waves (ramp-up, a narrowing tree): read again
                 // soon; otherwise every cfg.hunger batches
                 const uint32_t hg = cfg.nwaves > outst_cur ? cfg.nwaves - outst_cur : 0u;
@@ -984,6 +1192,21 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             }
             cyc_spill += __builtin_amdgcn_s_memtime() - ts;
         }
+        if constexpr (GLOBAL) {
+            // another rank is idle and no wave of this one is hungry: export
+            // the oldest items (one chunk per batch)
+            if (hungry == 0 && gidle > 0 && sz >= cfg.spill_lo) {
+                uint32_t n = (sz + 1) / 2;
+                if (n > pool.chunk) n = pool.chunk;
+                publish_pending<Kind, CAP>(pool, g, pend);
+                if (n > 0 && n < sz &&
+                    global_enqueue<Kind, CAP>(ctx, gv, pool.chunk * (uint32_t)Kind::kWords, st, bot, n, &g->err)) {
+                    bot += n;
+                    sz = top - bot;
+                    --gidle;
+                }
+            }
+        }
         if (HX_STAMPS && cfg.stamps) t_batch = __builtin_amdgcn_s_memtime();
     }
     publish_pending<Kind, CAP>(pool, g, pend);  // (error exits)
@@ -991,9 +1214,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
     if (busy_phase) cyc_busy += t_end - t_mark;
     else cyc_idle += t_end - t_mark;
-    if (active && lane == 0) {
+    if (active) {
         // only reached on an error break: keep the protocol consistent
-        __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+        wave_goes_idle<GLOBAL>(g, gv);
     }
     acc.flush(g);
     {

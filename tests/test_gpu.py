@@ -451,3 +451,32 @@ def test_atomic_calibration_shapes():
     hot, _ = H.atomic_calibrate(H.ATOMIC_HOT_WORD, 64)
     coal, _ = H.atomic_calibrate(H.ATOMIC_COALESCED32, 64)
     assert 0 < hot < scatter < coal
+
+
+# ------------------------------------------------ cross-GPU work sharing
+def test_cross_gpu_sharing_two_ranks_one_gpu():
+    """dist.GlobalPool: two ranks, one process each,
+    both on this GPU (gloo; the region in rank 0's HBM is mapped into rank
+    1's process over IPC exactly as between two GPUs). T1L split at depth 1
+    gives rank 0 two nodes and rank 1 the rest; sharing work must move
+    subtrees to rank 0 and keep the counts bit-exact; T3L (span-bound, its
+    busy rank always has hungry waves of its own) must stay exact too."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, REHEARSE_CASES="T1L:1,T3L:64", HCLIB_HIP_SPIN_LIMIT_MS="10000",
+               HCLIB_HIP_WAVES_PER_CU="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29547", "scripts/rehearse_global.py"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 4 and all(x["bit_exact"] for x in lines)
+    static, shared = lines[0], lines[1]
+    assert static["nodes_per_rank"][0] == 2 and not static["shared"]
+    assert shared["shared"] and shared["imported"][0] > 0 and shared["exported"][1] > 0
+    assert shared["nodes_per_rank"][0] > 1000 * static["nodes_per_rank"][0]
+    assert shared["active_after"] == 0 and shared["queued_after"] == 0
+    assert sum(shared["exported"]) == sum(shared["imported"])
