@@ -220,7 +220,17 @@ struct WaveStack {
     uint2 t1[CAP];                 // template words 4..5 (or 0..1)
     uint32_t mark[64];             // tagged group-start marks of the transposed push
     uint32_t stolen_from[8];       // chunks this wave took from each XCD's deques
+    // rarely-updated 64-bit sums kept out of the batch loop's SGPRs:
+    // [0] busy cycles, [1] idle cycles, [2] spill cycles, [3] narrow-loop
+    // cycles, [4] s_memtime at start, [5] s_memrealtime at start
+    unsigned long long cyc[6];
 };
+
+// lane 0 adds to a per-wave LDS sum (no return value, no wait)
+template <class WS>
+__device__ __forceinline__ void lds_sum(WS &st, int i, unsigned long long v) {
+    if (lane_id() == 0) __hip_atomic_fetch_add(&st.cyc[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
 
 template <class Kind, int CAP>
 __device__ __forceinline__ void load_tmpl(const WaveStack<Kind, CAP> &st, uint32_t slot, uint32_t *t) {
@@ -829,14 +839,17 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     bool active = false;
     uint32_t spins = 0;
     unsigned long long idle_since = 0;
-    unsigned long long nbatch = 0, npush = 0, nsteal = 0;
-    unsigned long long cyc_busy = 0, cyc_idle = 0, cyc_spill = 0, cyc_form = 0, cyc_proc = 0, cyc_push = 0;
+    // event counts fit 32 bits per wave (a wave runs < 2^32 batches); the
+    // 64-bit cycle sums and stamps stay 64-bit. Fewer live SGPR pairs: the
+    // batch loop's scalar state then spills less (v_writelane/readlane)
+    uint32_t nbatch = 0, npush = 0, nsteal = 0;
+    unsigned long long cyc_form = 0, cyc_proc = 0, cyc_push = 0;  // HX_STAMPS builds only
     uint32_t tag = 1;  // mark tags: 16 per batch
     for (int i = lane; i < kWaveSize; i += kWaveSize) st.mark[i] = 0;
     if (lane < 8) st.stolen_from[lane] = 0;
     uint32_t n_exec = 0, n_spawn = 0;          // per lane: tasks run, children created
-    unsigned long long items_stolen = 0;
-    unsigned long long n_narrow = 0, cyc_narrow = 0, n_narrow_in = 0;
+    uint32_t items_stolen = 0;
+    uint32_t n_narrow = 0, n_narrow_in = 0;
     // register carry: the previous batch's `carry` outputs, lane o holding
     // item o (template ctmpl, child index ck); they form the front of the
     // next batch instead of round-tripping through the LDS ring
@@ -872,7 +885,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     // s_memtime would wait for every LDS write of the batch); the per-phase
     // stamps of cfg.stamps are a diagnostic build that pays that wait
     unsigned long long t_mark = __builtin_amdgcn_s_memtime();
-    const unsigned long long t_begin = t_mark, rt_begin = __builtin_amdgcn_s_memrealtime();
+    if (lane < 6) st.cyc[lane] = 0;
+    if (lane == 0) {
+        st.cyc[4] = t_mark;
+        st.cyc[5] = __builtin_amdgcn_s_memrealtime();
+    }
     unsigned long long t_batch = t_mark;  // cfg.stamps only
     bool busy_phase = true;
     uint32_t outst_pf = 0;  // lane 0: `outstanding` as loaded one batch ago
@@ -889,7 +906,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             publish_pending<Kind, CAP>(pool, g, pend);
             if (busy_phase) {
                 const unsigned long long now = __builtin_amdgcn_s_memtime();
-                cyc_busy += now - t_mark;
+                lds_sum(st, 0, now - t_mark);
                 t_mark = now;
                 busy_phase = false;
             }
@@ -937,7 +954,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 active = true;
                 spins = 0;
                 const unsigned long long now = __builtin_amdgcn_s_memtime();
-                cyc_idle += now - t_mark;
+                lds_sum(st, 1, now - t_mark);
                 t_mark = now;
                 t_batch = now;
                 busy_phase = true;
@@ -1127,7 +1144,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     n_spawn = ns.n_spawn;
                     nbatch += lane0(ns.batches);
                     n_narrow += lane0(ns.batches);
-                    cyc_narrow += __builtin_amdgcn_s_memtime() - tn0;
+                    lds_sum(st, 3, __builtin_amdgcn_s_memtime() - tn0);
                     ++n_narrow_in;
                 }
                 continue;
@@ -1190,7 +1207,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 sz = top - bot;
                 if (hungry) --hungry;
             }
-            cyc_spill += __builtin_amdgcn_s_memtime() - ts;
+            lds_sum(st, 2, __builtin_amdgcn_s_memtime() - ts);
         }
         if constexpr (GLOBAL) {
             // another rank is idle and no wave of this one is hungry: export
@@ -1212,8 +1229,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     publish_pending<Kind, CAP>(pool, g, pend);  // (error exits)
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
     const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
-    if (busy_phase) cyc_busy += t_end - t_mark;
-    else cyc_idle += t_end - t_mark;
+    lds_sum(st, busy_phase ? 0 : 1, t_end - t_mark);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the LDS sums have landed
+    const unsigned long long cyc_busy = st.cyc[0], cyc_idle = st.cyc[1], cyc_spill = st.cyc[2],
+                             cyc_narrow = st.cyc[3], t_begin = st.cyc[4], rt_begin = st.cyc[5];
     if (active) {
         // only reached on an error break: keep the protocol consistent
         wave_goes_idle<GLOBAL>(g, gv);
@@ -1240,9 +1259,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         }
     }
     if (lane == 0 && n_narrow_in) {
-        add_agent(&g->narrow[0], n_narrow);
+        add_agent(&g->narrow[0], (unsigned long long)n_narrow);
         add_agent(&g->narrow[1], cyc_narrow);
-        add_agent(&g->narrow[2], n_narrow_in);
+        add_agent(&g->narrow[2], (unsigned long long)n_narrow_in);
     }
     if (lane == 0) {
         add_agent(&g->counters[kCtrBusyCycles], cyc_busy);
@@ -1254,9 +1273,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         add_agent(&g->counters[kCtrIdleCycles], cyc_idle);
         add_agent(&g->counters[kCtrSpillCycles], cyc_spill);
         add_agent(&g->counters[kCtrWaves], 1ull);
-        add_agent(&g->counters[kCtrBatches], nbatch);
-        add_agent(&g->counters[kCtrPushed], npush);
-        add_agent(&g->counters[kCtrStolen], nsteal);
+        add_agent(&g->counters[kCtrBatches], (unsigned long long)nbatch);
+        add_agent(&g->counters[kCtrPushed], (unsigned long long)npush);
+        add_agent(&g->counters[kCtrStolen], (unsigned long long)nsteal);
         add_agent(&g->counters[kCtrClockTicks], t_end - t_begin);
         add_agent(&g->counters[kCtrRealTicks], rt_end - rt_begin);
     }
