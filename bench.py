@@ -218,6 +218,18 @@ def load_pmc_traffic():
     return None
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo), for the baseline's provenance."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(threads, min_seconds=10.0):
     """Host-CPU HClib (oracle/ C restatement, "port") on T3L. Bounded sample:
     back-to-back full T3L searches until >= min_seconds of CPU-runtime time
@@ -236,7 +248,7 @@ def cpu_baseline(threads, min_seconds=10.0):
         total_s += sec.value
         searches += 1
     return {"value": T3L_GOLD[0] * searches / total_s, "unit": "nodes/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "sample": f"{searches} back-to-back full UTS T3L searches (111,345,631 nodes each) on "
                       f"oracle/hclib_cpu.c, {threads} worker threads, {total_s:.2f} s of search time"}
 
