@@ -230,7 +230,10 @@ struct UtsKind {
     static constexpr int kTmplWords = 6;
     static constexpr int kPieces = uts_pieces<CAP>();
     static constexpr int kWords = 8;
-    static constexpr bool kPure = FEAT != 1;  // the histogram's atomics are side effects (the trace stamps only from lane 0)
+    // every side effect (histogram atomics, trace stamps) is guarded by
+    // `counted` / lane 0, so invalid lanes may run the body: branch-free
+    // batches for every variant
+    static constexpr bool kPure = true;
     static constexpr bool kBoundedChildren = true;  // <= 100 (the root goes through roots())
     using Ctx = UtsCtx;
     struct Acc {
