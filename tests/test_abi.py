@@ -160,3 +160,25 @@ def test_sw_band_checks_arguments_then_needs_a_gpu():
     if not torch.cuda.is_available():
         with pytest.raises(H.HclibError):
             H.SwBand(s, s, 64, 64, 1, 3)
+
+
+def test_global_region_layout_and_no_gpu_failures():
+    """Cross-GPU sharing region (hclib_hip_global_*): its size is a host-side
+    function of the slot count (header + {seq, cnt} pairs + 2-KiB chunk
+    payloads), bad capacities are refused, and without a GPU the calls that
+    touch a device fail with an error instead of falling back."""
+    import torch
+
+    n = H.global_bytes(1024)
+    assert n >= 1024 * 8 + 1024 * 64 * 8 * 4 and n % 256 == 0
+    assert H.global_bytes(2048) - H.global_bytes(1024) == 1024 * (8 + 64 * 8 * 4)
+    with pytest.raises(H.HclibError):
+        H.global_bytes(1000)  # not a power of two
+    with pytest.raises(H.HclibError):
+        H.global_init(0, 1024, 2)  # no region
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(H.HclibError):
+        H.global_attach(None)
+    with pytest.raises(H.HclibError):
+        H.ipc_import(b"\0" * 64)
