@@ -111,9 +111,12 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     PoolView pool;
     HX_TRY(make_pool((uint32_t)env_int("HCLIB_HIP_DEQUES", 64),
                      (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
-                     (uint32_t)env_int("HCLIB_HIP_FIB_CHUNK", 8), FibKind::kWords, &pool));
+                     // 32-item chunks at 2 waves per CU: fib(30) 1.47 -> 0.92 ms
+                     // (profiles/r02/fib_knobs.log; 8-item chunks made the 2,048
+                     // idle-polling waves of the old default fight over crumbs)
+                     (uint32_t)env_int("HCLIB_HIP_FIB_CHUNK", 32), FibKind::kWords, &pool));
     const int grid = env_int("HCLIB_HIP_GRID", 0) > 0 ? env_int("HCLIB_HIP_GRID", 0)
-                                                    : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 4);
+                                                    : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 2);
     SchedConfig cfg;
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_HI", 256);
     // scripts/sweep_uts.py fib30 (profiles/r01_s5/knob_sweeps.log): 32 -> 1.50 ms, 2 -> 1.70 ms
