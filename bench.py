@@ -103,6 +103,10 @@ def skewed_sharing(H, rank, world, be, split=1):
         err = f"setup: {e}"
     if dist.max_over_ranks(1.0 if pool is None else 0.0, world, be) != 0.0:
         out["error"] = err or "setup failed on another rank"
+        try:
+            H.global_attach(None)  # (local: no collective on this path)
+        except Exception:  # noqa: BLE001
+            pass
         return out
     for shared in (False, True):
         if shared:

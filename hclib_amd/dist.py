@@ -275,14 +275,22 @@ class GlobalPool:
         self.backend = backend
         self._buf = None
         self._imported = None
+        # every rank takes part in the one broadcast whatever happens on rank
+        # 0 (a failed allocation or export sends None and every rank raises),
+        # so a caller's next collective is the same on all ranks
+        handle = [None]
         if rank == 0:
-            self._buf = torch.empty(H.global_bytes(cap), dtype=torch.uint8, device="cuda")
-            self.ptr = self._buf.data_ptr()
-            handle = [H.ipc_export(self.ptr)]
-        else:
-            handle = [None]
+            try:
+                self._buf = torch.empty(H.global_bytes(cap), dtype=torch.uint8, device="cuda")
+                self.ptr = self._buf.data_ptr()
+                handle = [H.ipc_export(self.ptr)]
+            except Exception as e:  # noqa: BLE001 (re-raised below, after the broadcast)
+                handle = [None]
+                self._err = e
         if world > 1:
             dist.broadcast_object_list(handle, src=0, group=group)
+        if handle[0] is None:
+            raise H.HclibError(f"cross-GPU region setup failed on rank 0: {getattr(self, '_err', '')}")
         if rank != 0:
             self._imported = H.ipc_import(handle[0])
             self.ptr = self._imported

@@ -155,3 +155,47 @@ def test_sw_band_and_block_split():
         dist.sw_bands(2, 3)
     with pytest.raises(ValueError):
         dist.sw_blocks(4, 0)
+
+
+# ------------------------------------------------ cross-GPU sharing leg
+# bench.py's N>1 work-sharing leg must never take the scaling run down: a
+# rank that cannot set the shared region up (here: no GPU at all) reports it
+# and every rank still reaches the same collectives, returning an error
+# record instead of raising or hanging.
+def _sharing_worker(rank, world, port, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    import hclib_amd as H
+    from hclib_amd import dist
+
+    r, w, _ = dist.init_from_env("gloo")
+    out = bench.skewed_sharing(H, r, w, "gloo")
+    dist.barrier(w, "gloo")
+    dist.shutdown(w)
+    q.put((r, out))
+
+
+def test_bench_work_sharing_leg_reports_setup_failure():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: the leg would run for real")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharing_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, out in res:
+        assert "error" in out and "static" not in out and "shared" not in out
+        assert out["workload"].startswith("test/uts T1L")
