@@ -312,32 +312,45 @@ struct UtsKind {
 };
 
 // GLOBAL: a sharded launch that shares work with the other ranks
-// (hclib_hip_global_attach; hx_sched.h GlobalView)
-template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512), bool GLOBAL = false>
-__global__ __launch_bounds__(64) void k_uts_search(UtsCtx ctx, PoolView pool, SchedGlobals *g,
-                                                   SchedConfig cfg) {
+// (hclib_hip_global_attach; hx_sched.h GlobalView). WPG: worker waves per
+// workgroup, handing work to idle siblings through LDS inboxes (hx_sched.h
+// Inbox) before the HBM deques.
+template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512), bool GLOBAL = false, int WPG = 1>
+__global__ __launch_bounds__(64 * WPG) void k_uts_search(UtsCtx ctx, PoolView pool, SchedGlobals *g,
+                                                         SchedConfig cfg) {
     constexpr int kUtsCap = CAP;
-    __shared__ WaveStack<UtsKind<MODE, FEAT, CAP>, kUtsCap> st;
+    using K = UtsKind<MODE, FEAT, CAP>;
+    __shared__ WaveStack<K, kUtsCap> st[WPG];
+    __shared__ Inbox<K> ib[WPG];
+    const uint32_t wave = WPG > 1 ? threadIdx.x / 64 : 0;
+    const uint32_t worker = blockIdx.x * WPG + wave;
+    if (WPG > 1) {
+        if (threadIdx.x < WPG) {
+            ib[threadIdx.x].state = 0;
+            ib[threadIdx.x].idle = 0;
+        }
+    }
     if (MODE == kUtsGeoFixed) {
         // table 0 in LDS for the rare tail search (uts_nc)
-        for (int i = threadIdx.x; i < 128; i += 64) s_thr[i] = ctx.thr[i];
-        __syncthreads();
+        for (int i = threadIdx.x; i < 128; i += 64 * WPG) s_thr[i] = ctx.thr[i];
+    }
+    if (MODE == kUtsRulesLds) {
+        // the per-node rule lookup becomes LDS-latency (no dependent HBM/L2 loads)
+        for (int i = threadIdx.x; i < ctx.nrules; i += 64 * WPG) s_rules[i] = ctx.rules[i];
+        for (int i = threadIdx.x; i < ctx.nthr; i += 64 * WPG) s_thr[i] = ctx.thr[i];
+    }
+    __syncthreads();
+    if (MODE == kUtsGeoFixed) {
         // the 16 thresholds compared per node live in VGPRs (wave-uniform
         // values the compiler would otherwise keep in SGPRs, spilling the
         // scheduler's scalar state around the batch loop)
         UtsCtx lc = ctx;
 #pragma unroll
         for (int k = 0; k < 16; ++k) asm volatile("v_mov_b32 %0, %1" : "=v"(lc.thr16[k]) : "s"(ctx.thr16[k]));
-        run_worker<UtsKind<MODE, FEAT, CAP>, kUtsCap, GLOBAL>(lc, pool, g, cfg, st, blockIdx.x == 0);
+        run_worker<K, kUtsCap, GLOBAL, WPG>(lc, pool, g, cfg, st[wave], worker == 0, ib, wave, worker);
         return;
     }
-    if (MODE == kUtsRulesLds) {
-        // the per-node rule lookup becomes LDS-latency (no dependent HBM/L2 loads)
-        for (int i = threadIdx.x; i < ctx.nrules; i += 64) s_rules[i] = ctx.rules[i];
-        for (int i = threadIdx.x; i < ctx.nthr; i += 64) s_thr[i] = ctx.thr[i];
-        __syncthreads();
-    }
-    run_worker<UtsKind<MODE, FEAT, CAP>, kUtsCap, GLOBAL>(ctx, pool, g, cfg, st, blockIdx.x == 0);
+    run_worker<K, kUtsCap, GLOBAL, WPG>(ctx, pool, g, cfg, st[wave], worker == 0, ib, wave, worker);
 }
 
 // ------------------------------------------------------ host: rules/tables
@@ -685,7 +698,18 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         if (ring == 256) kern = k_uts_search<kUtsGeoFixed, 0, 256>;
         else if (ring == 1024) kern = k_uts_search<kUtsGeoFixed, 0, 1024>;
     }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
+    // BIN trees: the two worker waves of a CU share a workgroup and hand work
+    // to each other through LDS before the HBM deques (T3L 34.0 -> 33.5-33.7
+    // ms, profiles/r02/inbox_ab.log; HCLIB_HIP_WPG = 1, 2 or 4)
+    int wpg = 1;
+    if (mode == kUtsBin && !global && !trace) {
+        wpg = env_int("HCLIB_HIP_WPG", 2);
+        if (wpg != 2 && wpg != 4) wpg = 1;
+        if (grid % wpg) wpg = 1;
+        if (wpg == 2) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 2> : k_uts_search<kUtsBin, 0, 1024, false, 2>;
+        if (wpg == 4) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 4> : k_uts_search<kUtsBin, 0, 1024, false, 4>;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid / wpg), dim3(64 * wpg), 0, m.stream, ctx, pool, m.globals, cfg);
     HX_HIP(hipGetLastError());
     HX_HIP(hipEventRecord(m.ev1, m.stream));
     SchedGlobals gl;

@@ -793,6 +793,77 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
     return ns;
 }
 
+// Sibling hand-off in LDS (workgroups of WPG > 1 worker waves). Every wave
+// of the workgroup has an inbox; a wave about to spill to the HBM deques
+// first offers the chunk to an idle sibling: it claims the sibling's empty
+// inbox (LDS CAS 0 -> 2), writes the items and sets it full (1) — LDS
+// operations of one wave land in issue order, so the items are there before
+// the flag. The idle sibling polls its own inbox before the deques. An inbox
+// chunk is not counted in `outstanding`: the taker counts itself back in
+// (+1) when it takes it, so a wave elsewhere may read 0 and leave while a
+// chunk is in flight here — it was idle anyway, and the taker and its
+// workgroup finish the work (the count can never go below the truth).
+template <class Kind>
+struct Inbox {
+    uint32_t state;  // 0 empty, 2 being filled, 1 full
+    uint32_t n;
+    uint32_t idle;   // the owner wave holds no work
+    uint32_t pad;
+    uint32_t w[64 * Kind::kWords];
+};
+
+template <class Kind, int CAP>
+__device__ bool inbox_put(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n) {
+    constexpr int W = Kind::kWords;
+    const int lane = lane_id();
+    uint32_t ok = 0;
+    if (lane == 0) {
+        uint32_t expect = 0u;
+        ok = __hip_atomic_compare_exchange_strong(&ib.state, &expect, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP)
+                 ? 1u
+                 : 0u;
+    }
+    if (!lane0(ok)) return false;
+    if ((uint32_t)lane < n) {
+        const uint32_t p = bot + (uint32_t)lane;
+        const uint2 dd = st.d[p & (CAP - 1)];
+        uint32_t w[W];
+        load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & (CAP - 1), w);
+        w[W - 2] = dd.x;
+        w[W - 1] = dd.y & (kMaxChildren - 1);
+#pragma unroll
+        for (int i = 0; i < W; ++i) ib.w[(uint32_t)lane * W + i] = w[i];
+    }
+    asm volatile("" ::: "memory");
+    if (lane == 0) {
+        *(volatile uint32_t *)&ib.n = n;
+        *(volatile uint32_t *)&ib.idle = 0u;
+        *(volatile uint32_t *)&ib.state = 1u;
+    }
+    return true;
+}
+
+// take a full inbox into the (empty) ring; returns the items (0: empty)
+template <class Kind, int CAP>
+__device__ uint32_t inbox_take(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st) {
+    constexpr int W = Kind::kWords;
+    const int lane = lane_id();
+    if (lane0(*(volatile uint32_t *)&ib.state) != 1u) return 0;
+    asm volatile("" ::: "memory");
+    const uint32_t n = lane0(*(volatile uint32_t *)&ib.n);
+    if ((uint32_t)lane < n) {
+        uint32_t w[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) w[i] = ib.w[(uint32_t)lane * W + i];
+        store_tmpl<Kind, CAP>(st, (uint32_t)lane, w);
+        st.d[lane] = make_uint2(w[W - 2], w[W - 1]);
+    }
+    asm volatile("" ::: "memory");
+    if (lane == 0) *(volatile uint32_t *)&ib.state = 0u;
+    return n;
+}
+
 // a wave stops holding work: local `outstanding` -1; the wave that takes it
 // to 0 releases its rank's unit of the global `active` (GLOBAL launches)
 template <bool GLOBAL>
@@ -813,9 +884,12 @@ __device__ __forceinline__ void wave_goes_idle(SchedGlobals *g, const GlobalView
 // (idle waves take chunks from the global ring, a wave holding spill_lo+
 // items exports a chunk while some rank is idle and none of its own waves
 // is hungry; termination waits for the global `active` count)
-template <class Kind, int CAP, bool GLOBAL = false>
+// WPG > 1: the workgroup's WPG worker waves hand work to each other through
+// LDS inboxes (`ib`: WPG of them, this wave's is ib[wave]; see Inbox)
+template <class Kind, int CAP, bool GLOBAL = false, int WPG = 1>
 __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, SchedGlobals *g,
-                           const SchedConfig &cfg, WaveStack<Kind, CAP> &st, bool seed_roots) {
+                           const SchedConfig &cfg, WaveStack<Kind, CAP> &st, bool seed_roots,
+                           Inbox<Kind> *ib = nullptr, uint32_t wave = 0, uint32_t worker = 0xffffffffu) {
     constexpr int TW = Kind::kTmplWords;
     constexpr uint32_t M = CAP - 1;
     constexpr int kPieces = pieces_of<Kind>();
@@ -825,7 +899,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     constexpr uint32_t kRoom = CAP - kGroupMax;
     static_assert(CAP >= kWaveSize * kGroupMax + kGroupMax, "ring must hold one batch's pushes");
     const int lane = lane_id();
-    const uint32_t gid = blockIdx.x;
+    const uint32_t gid = worker != 0xffffffffu ? worker : blockIdx.x;
     GlobalView gv;
     if constexpr (GLOBAL) gv = g->gview;
     uint32_t gidle_pf = 0, gidle = 0;  // GLOBAL: idle ranks, read with the hunger signal
@@ -913,6 +987,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             if (active) {
                 active = false;
                 wave_goes_idle<GLOBAL>(g, gv);
+                if constexpr (WPG > 1) {
+                    if (lane == 0) *(volatile uint32_t *)&ib[wave].idle = 1u;
+                }
             }
             // probe order: home, hint, then random (3/4 same XCD, 1/4 anywhere)
             uint32_t q = home;
@@ -925,7 +1002,16 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 uint32_t r = lane0(xorshift(rng));
                 q = ((r & 3) != 0) ? xcc * qpx + (r >> 2) % qpx : (r >> 2) % pool.nq;
             }
-            uint32_t n = dequeue_chunk<Kind, CAP>(pool, q, st, g);
+            uint32_t n = 0;
+            if constexpr (WPG > 1) {
+                n = inbox_take<Kind, CAP>(ib[wave], st);
+                if (n && lane == 0) add_agent(&g->outstanding, 1u);  // this wave holds work again
+                if (n) q = home;
+            }
+            if (n == 0) n = dequeue_chunk<Kind, CAP>(pool, q, st, g);
+            if constexpr (WPG > 1) {
+                if (n && lane == 0) *(volatile uint32_t *)&ib[wave].idle = 0u;
+            }
             if constexpr (GLOBAL) {
                 // every 4th probe that found nothing local: the global ring
                 if (n == 0 && (spins & 3) == 3) {
@@ -1196,7 +1282,16 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 if (n == 0 || n == sz) break;
                 // home deque first, then the other deques of this XCD slice
                 bool ok = false;
-                publish_pending<Kind, CAP>(pool, g, pend);  // one deferred chunk at a time
+                if constexpr (WPG > 1) {
+                    // an idle sibling of this workgroup first (LDS, no HBM round trip)
+                    for (uint32_t a = 1; a < (uint32_t)WPG && !ok; ++a) {
+                        Inbox<Kind> &sib = ib[(wave + a) % (uint32_t)WPG];
+                        if (lane0(*(volatile uint32_t *)&sib.idle) == 1u &&
+                            lane0(*(volatile uint32_t *)&sib.state) == 0u)
+                            ok = inbox_put<Kind, CAP>(sib, st, bot, n);
+                    }
+                }
+                if (!ok) publish_pending<Kind, CAP>(pool, g, pend);  // one deferred chunk at a time
                 for (uint32_t a = 0; a < qpx && !ok; ++a) {
                     const uint32_t q = xcc * qpx + (home - xcc * qpx + a) % qpx;
                     ok = enqueue_chunk<Kind, CAP>(pool, g, q, st, bot, n, occ, cfg.defer ? &pend : nullptr);
