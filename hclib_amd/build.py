@@ -36,7 +36,9 @@ CFLAGS = [
 
 
 VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "strict": ["-DHX_STRICT_HANDOFF=1"],
-            "narrow_noinline": ["-DHX_NARROW_NOINLINE=1"]}
+            "narrow_noinline": ["-DHX_NARROW_NOINLINE=1"],
+            "sched_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
+            "sched_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 
 
 def _hash(paths, cflags):
