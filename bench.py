@@ -132,7 +132,8 @@ def skewed_sharing(H, rank, world, be, split=1):
                     "kernel_ms_per_rank": dist.gather_floats(r["kernel_ms"], world, be)}
     if "error" not in out:
         g = pool.read()
-        out["shared"].update({"chunks_exported": g["exported"][:world], "chunks_imported": g["imported"][:world]})
+        out["shared"].update({"chunks_exported": g["exported"][:world], "chunks_imported": g["imported"][:world],
+                              "region_memory": pool.mem_kind})
         out["speedup"] = out["static"]["ms"] / out["shared"]["ms"]
     H.global_attach(None)
     pool.close()

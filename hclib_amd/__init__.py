@@ -122,6 +122,8 @@ def lib():
         L.hclib_hip_global_bytes.restype = C.c_size_t
         L.hclib_hip_global_bytes.argtypes = [C.c_uint32]
         L.hclib_hip_global_init.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
+        L.hclib_hip_global_alloc.argtypes = [C.c_uint32, C.c_int, C.POINTER(C.c_void_p)]
+        L.hclib_hip_global_free.argtypes = [C.c_void_p]
         L.hclib_hip_global_attach.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
         L.hclib_hip_global_read.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.hclib_hip_ipc_export.argtypes = [C.c_void_p, C.c_void_p]
@@ -221,6 +223,21 @@ def global_bytes(cap: int) -> int:
     if n == 0:
         raise HclibError("global_bytes: cap must be a power of two >= 2")
     return n
+
+
+GLOBAL_MEM_KINDS = {"uncached": 0, "fine": 1, "device": 2}
+
+
+def global_alloc(cap: int, kind: str = "uncached") -> int:
+    """Allocate a work-sharing region (hclib_hip_global_alloc); kind is one of
+    GLOBAL_MEM_KINDS."""
+    p = C.c_void_p()
+    _check(lib().hclib_hip_global_alloc(cap, GLOBAL_MEM_KINDS[kind], C.byref(p)), "hclib_hip_global_alloc")
+    return p.value
+
+
+def global_free(region: Optional[int]) -> None:
+    _check(lib().hclib_hip_global_free(region), "hclib_hip_global_free")
 
 
 def global_init(region: int, cap: int, nranks: int) -> None:

@@ -396,6 +396,37 @@ extern "C" int hclib_hip_global_read(const void *region, uint64_t out[3 + 2 * kG
     return HCLIB_HIP_OK;
 }
 
+// The region's memory: uncached device memory (kind 0: every access, local
+// or over xGMI, goes to the owner's HBM, the coherence a region that several
+// GPUs update inside their kernels needs), fine-grained (kind 1) or plain
+// coarse-grained hipMalloc (kind 2, coherent at system scope on one GPU).
+// Allocated here rather than through a caching allocator so the IPC handle
+// names exactly this allocation (no sub-allocation offset).
+extern "C" int hclib_hip_global_alloc(uint32_t cap, int kind, void **region_out) {
+    size_t co, dof;
+    if (!region_out || cap < 2 || (cap & (cap - 1)) || kind < 0 || kind > 2) {
+        set_error("hclib_hip_global_alloc: invalid arguments");
+        return HCLIB_HIP_EINVAL;
+    }
+    *region_out = nullptr;
+    HX_TRY(ensure_device());
+    const size_t bytes = global_layout(cap, &co, &dof);
+    if (kind == 2) {
+        HX_HIP(hipMalloc(region_out, bytes));
+    } else {
+        HX_HIP(hipExtMallocWithFlags(region_out, bytes,
+                                     kind == 0 ? hipDeviceMallocUncached : hipDeviceMallocFinegrained));
+    }
+    return HCLIB_HIP_OK;
+}
+
+extern "C" int hclib_hip_global_free(void *region) {
+    if (!region) return HCLIB_HIP_OK;
+    HX_TRY(ensure_device());
+    HX_HIP(hipFree(region));
+    return HCLIB_HIP_OK;
+}
+
 extern "C" int hclib_hip_ipc_export(void *dev_ptr, void *handle_out) {
     if (!dev_ptr || !handle_out) {
         set_error("hclib_hip_ipc_export: invalid arguments");

@@ -266,7 +266,6 @@ class GlobalPool:
     (default: the world group)."""
 
     def __init__(self, rank: int, world: int, backend: str = "nccl", cap: int = 1024, group=None):
-        import torch
         import torch.distributed as dist
 
         import hclib_amd as H
@@ -278,22 +277,37 @@ class GlobalPool:
         # every rank takes part in the one broadcast whatever happens on rank
         # 0 (a failed allocation or export sends None and every rank raises),
         # so a caller's next collective is the same on all ranks
+        # The region is uncached device memory when the driver grants it and
+        # IPC exports it (every access from any GPU then reaches rank 0's
+        # HBM), else fine-grained, else plain device memory; `mem_kind` says
+        # which (HCLIB_GLOBAL_MEM picks one).
         handle = [None]
+        self.mem_kind = None
         if rank == 0:
-            try:
-                self._buf = torch.empty(H.global_bytes(cap), dtype=torch.uint8, device="cuda")
-                self.ptr = self._buf.data_ptr()
-                handle = [H.ipc_export(self.ptr)]
-            except Exception as e:  # noqa: BLE001 (re-raised below, after the broadcast)
-                handle = [None]
-                self._err = e
+            errs = []
+            kinds = [os.environ["HCLIB_GLOBAL_MEM"]] if os.environ.get("HCLIB_GLOBAL_MEM") else \
+                ["uncached", "fine", "device"]
+            for kind in kinds:
+                p = None
+                try:
+                    p = H.global_alloc(cap, kind)
+                    handle = [(H.ipc_export(p), kind)]
+                    self._buf, self.ptr, self.mem_kind = p, p, kind
+                    break
+                except Exception as e:  # noqa: BLE001 (re-raised below, after the broadcast)
+                    errs.append(f"{kind}: {e}")
+                    if p:
+                        H.global_free(p)
+            if handle[0] is None:
+                self._err = "; ".join(errs)
         if world > 1:
             dist.broadcast_object_list(handle, src=0, group=group)
         if handle[0] is None:
             raise H.HclibError(f"cross-GPU region setup failed on rank 0: {getattr(self, '_err', '')}")
         if rank != 0:
-            self._imported = H.ipc_import(handle[0])
+            self._imported = H.ipc_import(handle[0][0])
             self.ptr = self._imported
+            self.mem_kind = handle[0][1]
         H.global_attach(self.ptr, cap, rank)
 
     def _barrier(self):
@@ -326,4 +340,6 @@ class GlobalPool:
             H.ipc_close(self._imported)
             self._imported = None
         self._barrier()
-        self._buf = None
+        if self._buf is not None:
+            H.global_free(self._buf)
+            self._buf = None

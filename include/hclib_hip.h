@@ -266,8 +266,13 @@ int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int shard, int ns
  * each rank's launch ends only when no rank holds work (the region's
  * `active` count, system-scope atomics). hclib_hip_global_read fills
  * out[0] active, out[1] idle ranks, out[2] chunks queued, then per rank r
- * out[3 + 2r] chunks exported and out[4 + 2r] chunks imported (r < 16). */
+ * out[3 + 2r] chunks exported and out[4 + 2r] chunks imported (r < 16).
+ * hclib_hip_global_alloc allocates the region itself (kind 0 uncached device
+ * memory, 1 fine-grained, 2 plain hipMalloc; free with hclib_hip_global_free)
+ * so that its IPC handle names exactly that allocation. */
 size_t hclib_hip_global_bytes(uint32_t cap);
+int hclib_hip_global_alloc(uint32_t cap, int kind, void **region_out);
+int hclib_hip_global_free(void *region);
 int hclib_hip_global_init(void *region, uint32_t cap, int nranks);
 int hclib_hip_global_attach(void *region, uint32_t cap, int rank);
 int hclib_hip_global_read(const void *region, uint64_t out[35]);

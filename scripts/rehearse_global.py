@@ -48,6 +48,7 @@ def main():
             ok = ok and exact
             if rank == 0:
                 line = {"tree": name, "split": int(split), "ranks": world, "shared": shared, "bit_exact": exact,
+                        "region_memory": pool.mem_kind,
                         "nodes_per_rank": [int(n) for n in nodes], "kernel_ms_per_rank": kms}
                 if g:
                     line.update({"exported": g["exported"][:world], "imported": g["imported"][:world],

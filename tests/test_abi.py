@@ -176,9 +176,13 @@ def test_global_region_layout_and_no_gpu_failures():
         H.global_bytes(1000)  # not a power of two
     with pytest.raises(H.HclibError):
         H.global_init(0, 1024, 2)  # no region
+    with pytest.raises(KeyError):
+        H.global_alloc(1024, "host")  # no such region memory
     if torch.cuda.is_available():
         pytest.skip("a GPU is present")
     with pytest.raises(H.HclibError):
         H.global_attach(None)
     with pytest.raises(H.HclibError):
         H.ipc_import(b"\0" * 64)
+    with pytest.raises(H.HclibError):
+        H.global_alloc(1024)

@@ -480,3 +480,4 @@ def test_cross_gpu_sharing_two_ranks_one_gpu():
     assert shared["nodes_per_rank"][0] > 1000 * static["nodes_per_rank"][0]
     assert shared["active_after"] == 0 and shared["queued_after"] == 0
     assert sum(shared["exported"]) == sum(shared["imported"])
+    assert shared["region_memory"] == os.environ.get("HCLIB_GLOBAL_MEM", "uncached")
