@@ -382,6 +382,20 @@ static int geo_n(double prob, uint32_t h) {
     return cvt_int_x86(floor(log(1 - u) / log(1 - prob)));
 }
 
+// Expected node count of a GEO / HYBRID tree (sum over depths of the product
+// of the mean branching factors above it) — a launch-shape heuristic only:
+// T1 1.4 M, T2 0.8 M, T4 3.3 M, T5 3.8 M, T1L 89 M, T2L 184 M
+static double uts_expected_nodes(const hclib_hip_uts_params_t &p) {
+    double tot = 0.0, prod = 1.0;
+    for (int d = 0; d < 10 * p.gen_mx + 10 && prod > 1e-9 && tot < 1e13; ++d) {
+        tot += prod;
+        const bool bin_level = p.type == 0 ? d > 0 : (p.type == 2 && d >= p.shift_depth * p.gen_mx);
+        const double mu = bin_level ? p.non_leaf_prob * p.non_leaf_bf : geo_bi(p, d);
+        prod *= mu > 0.0 ? mu : 0.0;
+    }
+    return tot;
+}
+
 struct UtsTables {
     std::vector<int4> rules;
     std::vector<uint32_t> thr;  // 128 words per geo table
@@ -634,11 +648,14 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // small tree (T1, ~4 M nodes in 1 ms) loses more to spreading its few
     // first levels over 2048 waves than it gains (profiles/r02/
     // sweep_t1xl_waves_geo.log: T1XL 90 -> 52 ms from 4 to 8, T1 1.0 ->
-    // 1.45 ms). Size estimate: b_0^gen_mx nodes for the fixed shape.
+    // 1.45 ms). Size: uts_expected_nodes.
+    // Rule-table trees (other shapes, HYBRID) of a few million nodes run
+    // fastest with 4 (T2 1.80 -> 1.36 ms, T4 1.05 -> 0.86, T5 1.07 -> 0.96;
+    // T2L still wants 8: profiles/r02/geo_spill.log)
     int wpc_default = 2, ring_default = 512;
     if (!bin) {
-        const double est = (params->type == 1 && params->shape_fn == 3) ? pow(params->b_0, (double)params->gen_mx) : 1e9;
-        wpc_default = est >= 3e7 ? 8 : 2;
+        const double est = uts_expected_nodes(*params);
+        wpc_default = est >= 3e7 ? 8 : (geo_fixed ? 2 : 4);
         // and a small tree runs faster on 256-item rings (one piece per task:
         // the frontier fans out by range splitting) at 2 waves per CU: T1
         // 0.98 -> 0.70 ms; a large one slower (T1XL 52 -> 70 ms),
@@ -652,8 +669,14 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_SPILL_HI", 512);
     // BIN trees with the narrow-frontier loop give work away from 72 items
     // (just over one batch: a wave keeps at most ~one batch of a narrow
-    // frontier, T3L 36.3 -> 35.0 ms, profiles/r02/t3l_knobs.log); GEO at 96
-    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", bin ? 72 : 96);
+    // frontier, T3L 36.3 -> 35.0 ms, profiles/r02/t3l_knobs.log). GEO trees
+    // keep far more before feeding hungry waves (fewer, fuller hand-offs;
+    // profiles/r02/geo_spill.log): 336 on the fixed-shape 512-item rings (T1L
+    // 5.57 -> 4.37 ms, T1XL 53.5 -> 51.4 ms), 224 with rule tables (T2 2.82 ->
+    // 1.71 ms, T5 1.40 -> 1.00, T2L 6.33 -> 5.20), 128 on 256-item rings (T1)
+    const int ring_used = geo_fixed && !(nshards > 1 || max_levels > 0) ? env_int("HCLIB_HIP_UTS_RING", ring_default) : 512;
+    const int spill_lo_default = bin ? 72 : !geo_fixed ? 224 : ring_used >= 512 ? 336 : 128;
+    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", spill_lo_default);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);

@@ -10,7 +10,12 @@ import hclib_amd as H  # noqa: E402
 
 TREES = {"T1": ("-t 1 -a 3 -d 10 -b 4 -r 19", 4130071),
          "T3L": ("-t 0 -b 2000 -q 0.200014 -m 5 -r 7", 111345631),
-         "T1XL": ("-t 1 -a 3 -d 15 -b 4 -r 29", 1635119272), "fib30": ("fib", 0)}
+         "T1XL": ("-t 1 -a 3 -d 15 -b 4 -r 29", 1635119272), "fib30": ("fib", 0),
+         "T1L": ("-t 1 -a 3 -d 13 -b 4 -r 29", 102181082)}
+if sys.argv[1] not in TREES:  # any published tree (tests/golden/uts_goldens.json)
+    import json
+    pub = json.load(open(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "uts_goldens.json")))
+    TREES[sys.argv[1]] = (pub["published"][sys.argv[1]]["args"], pub["published"][sys.argv[1]]["nodes"])
 args, nodes = TREES[sys.argv[1]]
 knobs = [(k, v.split(",")) for k, v in (a.split("=") for a in sys.argv[2:])]
 H.init(0)
