@@ -682,7 +682,9 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
     // hunger read every 32 batches, every 8 while many waves are hungry
     // (scripts/sweep_uts.py: T1 1.37 -> 1.07 ms, T1XL 101 -> 97 ms, T3L even)
-    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", 32);
+    // (fixed-shape GEO trees on 512-item rings every 64: T1XL 51.5 -> 49.9 ms,
+    // T1L even, T2L slower; profiles/r02/geo_knobs.log)
+    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", geo_fixed && ring_used >= 512 ? 64 : 32);
     cfg.hunger_fast = (uint32_t)env_int("HCLIB_HIP_HUNGER_FAST", 0);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
     cfg.backoff = (uint32_t)env_int("HCLIB_HIP_BACKOFF", 16);
