@@ -214,10 +214,23 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
 
 // ring items per wave (CAP) and the pieces a task's children are pushed as:
 // BIN trees 1024 / 8 (m <= 8 children keep every batch uniform: the register
-// carry); GEO trees 512 / 5 by default (16 KiB: 8 waves per CU resident),
-// 256 / 1 (8 KiB) and 1024 / 8 as measured alternatives (HCLIB_HIP_UTS_RING)
-template <int CAP>
-constexpr int uts_pieces() { return CAP >= 1024 ? 8 : (CAP >= 512 ? 5 : 1); }
+// carry); GEO trees 512 by default (16 KiB: 8 waves per CU resident), 256 / 1
+// (8 KiB) and 1024 / 8 as measured alternatives (HCLIB_HIP_UTS_RING). On 512
+// rings a fixed-shape GEO tree pushes a task's children as ONE range item
+// (the residual splits in halves as it is popped): fewer ring writes and a
+// one-iteration push loop, T1XL 49.7 -> 37.6 ms, T1L 4.48 -> 4.04, against
+// 5 pieces (45.0 / 4.17 at 3, 42.3 / 4.43 at 2); rule-table trees keep 5
+// (T4 0.88 -> 2.35 ms at 1, T2 1.37 -> 1.65): profiles/r02/pieces_ab.log
+#ifndef HX_UTS_PIECES_512
+#define HX_UTS_PIECES_512 5
+#endif
+#ifndef HX_UTS_FIXED_PIECES_512
+#define HX_UTS_FIXED_PIECES_512 1
+#endif
+template <int MODE, int CAP>
+constexpr int uts_pieces() {
+    return CAP >= 1024 ? 8 : (CAP >= 512 ? (MODE == kUtsGeoFixed ? HX_UTS_FIXED_PIECES_512 : HX_UTS_PIECES_512) : 1);
+}
 
 // FEAT = 0: plain search; 1: sharded (nshards > 1) and/or per-level histogram;
 // 2: diagnostic trace (HCLIB_HIP_UTS_TRACE=1): per depth, the earliest
@@ -228,7 +241,7 @@ template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512)>
 struct UtsKind {
     // template = the node {state[5], height}; an item = its children [k, kend)
     static constexpr int kTmplWords = 6;
-    static constexpr int kPieces = uts_pieces<CAP>();
+    static constexpr int kPieces = uts_pieces<MODE, CAP>();
     static constexpr int kWords = 8;
     // every side effect (histogram atomics, trace stamps) is guarded by
     // `counted` / lane 0, so invalid lanes may run the body: branch-free
@@ -671,11 +684,12 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // (just over one batch: a wave keeps at most ~one batch of a narrow
     // frontier, T3L 36.3 -> 35.0 ms, profiles/r02/t3l_knobs.log). GEO trees
     // keep far more before feeding hungry waves (fewer, fuller hand-offs;
-    // profiles/r02/geo_spill.log): 336 on the fixed-shape 512-item rings (T1L
-    // 5.57 -> 4.37 ms, T1XL 53.5 -> 51.4 ms), 224 with rule tables (T2 2.82 ->
-    // 1.71 ms, T5 1.40 -> 1.00, T2L 6.33 -> 5.20), 128 on 256-item rings (T1)
+    // profiles/r02/geo_spill.log): 224 with rule tables (T2 2.82 -> 1.71 ms,
+    // T5 1.40 -> 1.00, T2L 6.33 -> 5.20) and on the fixed-shape 512-item rings
+    // at one piece per task (T1XL 37.2 ms, T1L 3.77; profiles/r02/
+    // pieces_tune.log; 336 at five pieces), 128 on 256-item rings (T1)
     const int ring_used = geo_fixed && !(nshards > 1 || max_levels > 0) ? env_int("HCLIB_HIP_UTS_RING", ring_default) : 512;
-    const int spill_lo_default = bin ? 72 : !geo_fixed ? 224 : ring_used >= 512 ? 336 : 128;
+    const int spill_lo_default = bin ? 72 : !geo_fixed ? 224 : ring_used >= 512 ? 224 : 128;
     cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", spill_lo_default);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
