@@ -40,7 +40,8 @@ VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "strict": ["-DHX_STRICT_HANDOFF=1"],
             "sched_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
             "sched_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
             # GEO 512-ring piece counts (uts.hip uts_pieces): fixed-shape trees at 5, rule tables at 1
-            "fixed_pieces5": ["-DHX_UTS_FIXED_PIECES_512=5"], "rules_pieces1": ["-DHX_UTS_PIECES_512=1"]}
+            "fixed_pieces5": ["-DHX_UTS_FIXED_PIECES_512=5"], "rules_pieces1": ["-DHX_UTS_PIECES_512=1"],
+            "residual_whole": ["-DHX_RESIDUAL_WHOLE=1"]}
 
 
 def _hash(paths, cflags):

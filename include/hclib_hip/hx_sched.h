@@ -196,6 +196,13 @@ struct SchedConfig {
 // smaller ring (one batch pushes at most 64 * (pieces + 2) items), so a
 // kind with wide nodes can trade residual splitting for LDS, i.e. for more
 // resident waves per CU.
+// A popped range item's residual (children k+1..kend-1) goes back as two
+// halves (default: a wide node's children spread over more batches sooner)
+// or, with HX_RESIDUAL_WHOLE=1 (a measured alternative), as one item
+#ifndef HX_RESIDUAL_WHOLE
+#define HX_RESIDUAL_WHOLE 0
+#endif
+
 template <class K, class = void>
 struct KindPieces {
     static constexpr int value = 8;
@@ -1160,7 +1167,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         top -= take_ring;
         // ---- push: residual range of the item + the new task's children
         const uint32_t rlen = has ? kend - k - 1u : 0u;
-        const uint32_t nres = rlen == 0 ? 0u : (rlen == 1 ? 1u : 2u);
+        const uint32_t nres = rlen == 0 ? 0u : (rlen == 1 || HX_RESIDUAL_WHOLE ? 1u : 2u);
         uint32_t ucnt = cnt > 0 ? (uint32_t)cnt : 0u;
         n_exec += has ? 1u : 0u;
         n_spawn += has ? ucnt : 0u;
