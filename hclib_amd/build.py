@@ -41,7 +41,9 @@ VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "strict": ["-DHX_STRICT_HANDOFF=1"],
             "sched_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
             # GEO 512-ring piece counts (uts.hip uts_pieces): fixed-shape trees at 5, rule tables at 1
             "fixed_pieces5": ["-DHX_UTS_FIXED_PIECES_512=5"], "rules_pieces1": ["-DHX_UTS_PIECES_512=1"],
-            "residual_whole": ["-DHX_RESIDUAL_WHOLE=1"]}
+            "residual_whole": ["-DHX_RESIDUAL_WHOLE=1"],
+            "split3": ["-DHX_RESIDUAL_SPLIT_MIN=3"], "split4": ["-DHX_RESIDUAL_SPLIT_MIN=4"],
+            "split8": ["-DHX_RESIDUAL_SPLIT_MIN=8"]}
 
 
 def _hash(paths, cflags):

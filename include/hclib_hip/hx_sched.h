@@ -202,6 +202,10 @@ struct SchedConfig {
 #ifndef HX_RESIDUAL_WHOLE
 #define HX_RESIDUAL_WHOLE 0
 #endif
+// (a residual shorter than HX_RESIDUAL_SPLIT_MIN children stays whole)
+#ifndef HX_RESIDUAL_SPLIT_MIN
+#define HX_RESIDUAL_SPLIT_MIN 2
+#endif
 
 template <class K, class = void>
 struct KindPieces {
@@ -1167,7 +1171,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         top -= take_ring;
         // ---- push: residual range of the item + the new task's children
         const uint32_t rlen = has ? kend - k - 1u : 0u;
-        const uint32_t nres = rlen == 0 ? 0u : (rlen == 1 || HX_RESIDUAL_WHOLE ? 1u : 2u);
+        const uint32_t nres = rlen == 0 ? 0u : (rlen < (uint32_t)HX_RESIDUAL_SPLIT_MIN || HX_RESIDUAL_WHOLE ? 1u : 2u);
         uint32_t ucnt = cnt > 0 ? (uint32_t)cnt : 0u;
         n_exec += has ? 1u : 0u;
         n_spawn += has ? ucnt : 0u;
