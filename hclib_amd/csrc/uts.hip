@@ -651,8 +651,6 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     const uint32_t nq = (uint32_t)env_int("HCLIB_HIP_DEQUES", 64);
     HX_TRY(make_pool(nq, (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
                      (uint32_t)env_int("HCLIB_HIP_CHUNK", 64), UtsKind<kUtsBin, 0>::kWords, &pool));
-    // span-bound BIN trees run fastest with 2 waves per CU (fewer idle pollers,
-    // fewer hand-offs); throughput-bound GEO trees with 4
     const bool bin = params->type == 0 && T.rules.size() == 2 && T.rules[1].x == 1 && T.stationary;
     const bool geo_fixed = !bin && geo_depth > 0 && env_int("HCLIB_HIP_UTS_GEO_FIXED", 1);
     // waves per CU: span-bound BIN trees run fastest with 2 (fewer idle
@@ -689,7 +687,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // at one piece per task (T1XL 37.2 ms, T1L 3.77; profiles/r02/
     // pieces_tune.log; 336 at five pieces), 128 on 256-item rings (T1)
     const int ring_used = geo_fixed && !(nshards > 1 || max_levels > 0) ? env_int("HCLIB_HIP_UTS_RING", ring_default) : 512;
-    const int spill_lo_default = bin ? 72 : !geo_fixed ? 224 : ring_used >= 512 ? 224 : 128;
+    const int spill_lo_default = bin ? 72 : (geo_fixed && ring_used < 512) ? 128 : 224;
     cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", spill_lo_default);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
