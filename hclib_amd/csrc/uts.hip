@@ -598,21 +598,41 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     }
     HX_TRY(ensure_device());
     Module &m = mod();
-    UtsTables T;
-    HX_TRY(build_tables(*params, T));
+    // The rule / threshold tables are pure functions of the parameters and
+    // cost ~1 ms of libm on the host for a GEO tree (100 threshold searches
+    // per depth): the last set and its device copy are kept for the next
+    // search of the same tree (every call returns with the stream drained, so
+    // no launch still reads them when they are replaced)
+    static struct {
+        bool have = false;
+        int device = -1;
+        hclib_hip_uts_params_t p;
+        UtsTables T;
+        void *dmem = nullptr;
+    } tab;
+    if (!tab.have || tab.device != m.device || memcmp(&tab.p, params, sizeof(tab.p)) != 0) {
+        if (tab.dmem && tab.device == m.device) (void)hipFree(tab.dmem);
+        tab.have = false;
+        tab.dmem = nullptr;
+        HX_TRY(build_tables(*params, tab.T));
+        const size_t rb = tab.T.rules.size() * sizeof(int4), tb = tab.T.thr.size() * 4;
+        HX_HIP(hipMalloc(&tab.dmem, ((rb + 255) & ~(size_t)255) + tb + 256));
+        char *dp = (char *)tab.dmem;
+        HX_HIP(hipMemcpy(dp, tab.T.rules.data(), rb, hipMemcpyHostToDevice));
+        HX_HIP(hipMemcpy(dp + ((rb + 255) & ~(size_t)255), tab.T.thr.data(), tb, hipMemcpyHostToDevice));
+        tab.p = *params;
+        tab.device = m.device;
+        tab.have = true;
+    }
+    const UtsTables &T = tab.T;
+    int4 *d_rules = (int4 *)tab.dmem;
+    uint32_t *d_thr = (uint32_t *)((char *)tab.dmem + ((T.rules.size() * sizeof(int4) + 255) & ~(size_t)255));
 
-    // device copies of the rule tables (+ optional histogram)
-    const size_t rb = T.rules.size() * sizeof(int4), tb = T.thr.size() * 4,
-                 hb = (size_t)max_levels * 8;
+    // the optional per-level histogram
+    const size_t hb = (size_t)max_levels * 8;
     void *dmem = nullptr;
-    HX_HIP(hipMalloc(&dmem, rb + tb + hb + 512));
-    char *dp = (char *)dmem;
-    int4 *d_rules = (int4 *)dp;
-    uint32_t *d_thr = (uint32_t *)(dp + ((rb + 255) & ~(size_t)255));
-    unsigned long long *d_hist =
-        (unsigned long long *)(dp + ((rb + 255) & ~(size_t)255) + ((tb + 255) & ~(size_t)255));
-    HX_HIP(hipMemcpyAsync(d_rules, T.rules.data(), rb, hipMemcpyHostToDevice, m.stream));
-    HX_HIP(hipMemcpyAsync(d_thr, T.thr.data(), tb, hipMemcpyHostToDevice, m.stream));
+    if (max_levels) HX_HIP(hipMalloc(&dmem, hb));
+    unsigned long long *d_hist = (unsigned long long *)dmem;
     const bool trace = env_int("HCLIB_HIP_UTS_TRACE", 0) != 0 && max_levels > 0;
     if (max_levels) HX_HIP(hipMemsetAsync(d_hist, trace ? 0xff : 0, hb, m.stream));
 
