@@ -95,11 +95,12 @@ def build(verbose: bool = True, variant: str = "") -> str:
         os.replace(lib + ".tmp", lib)
         with open(stamp, "w") as f:
             f.write(key)
-    # drop stale objects
+    # drop stale objects, and the per-object offload-bundle files the link
+    # step leaves beside the library (libhclib_amd.so.<n>.<target>)
     keep = set(objs)
     for f in os.listdir(out):
         p = os.path.join(out, f)
-        if f.endswith(".o") and p not in keep:
+        if (f.endswith(".o") and p not in keep) or f.startswith("libhclib_amd.so."):
             os.remove(p)
     if verbose:
         print("built", lib)
