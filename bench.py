@@ -235,10 +235,68 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(threads, min_seconds=10.0):
-    """Host-CPU HClib (oracle/ C restatement, "port") on T3L. Bounded sample:
-    back-to-back full T3L searches until >= min_seconds of CPU-runtime time
-    (about 10-12 s at 16 threads); value = all nodes searched / total time."""
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def cpu_allotment():
+    """What this process may actually run on, with the evidence: the affinity
+    mask, the cgroup CPU quota (v2 cpu.max or v1 cfs_quota/period of this
+    process's cpu cgroup), the cpuset, and the job's designated share
+    (OMP_NUM_THREADS, which the GPU box sets to the lease's CPU share). The
+    worker count the reference would use is HCLIB_WORKERS or nprocs
+    (src/hclib-locality-graph.c:585-595); here the baseline uses the CPUs the
+    process is allowed, i.e. min(affinity, quota), further limited to the
+    designated share only if one is set, and says which bound applied."""
+    aff = len(os.sched_getaffinity(0))
+    quota, qsrc = None, None
+    cg = {}
+    for line in (_read("/proc/self/cgroup") or "").splitlines():
+        parts = line.split(":", 2)
+        if len(parts) == 3:
+            for ctl in parts[1].split(",") or [""]:
+                cg[ctl] = parts[2]
+    v2 = _read(f"/sys/fs/cgroup{cg.get('', '/')}/cpu.max".replace("//", "/")) or _read("/sys/fs/cgroup/cpu.max")
+    if v2:
+        q, per = (v2.split() + ["100000"])[:2]
+        qsrc = f"cgroup v2 cpu.max = {v2!r}"
+        if q != "max":
+            quota = int(q) / int(per)
+    else:
+        base = "/sys/fs/cgroup/cpu" + (cg.get("cpu", "/") if cg.get("cpu", "/") != "/" else "")
+        q, per = _read(base + "/cpu.cfs_quota_us"), _read(base + "/cpu.cfs_period_us")
+        if q is not None and per is not None:
+            qsrc = f"cgroup v1 {base}/cpu.cfs_quota_us = {q}, cfs_period_us = {per}"
+            if int(q) > 0:
+                quota = int(q) / int(per)
+    cpuset = None
+    for path in ("/sys/fs/cgroup/cpuset.cpus.effective", "/sys/fs/cgroup/cpuset/cpuset.effective_cpus",
+                 "/sys/fs/cgroup/cpuset/cpuset.cpus"):
+        cpuset = _read(path)
+        if cpuset:
+            break
+    allowed = aff if quota is None else max(1, min(aff, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    override = os.environ.get("HCLIB_BENCH_CPU_THREADS")
+    if override:
+        threads, source = max(1, int(override)), "HCLIB_BENCH_CPU_THREADS"
+    elif omp and 0 < int(omp) < allowed:
+        threads, source = int(omp), (f"OMP_NUM_THREADS={omp}: the job's designated CPU share, below the "
+                                     f"{allowed} CPUs affinity/quota would allow")
+    else:
+        threads, source = allowed, ("cgroup quota" if quota is not None and int(quota) < aff else "affinity mask")
+    return {"affinity_cpus": aff, "cgroup_quota": quota, "cgroup_source": qsrc, "cpuset": cpuset,
+            "omp_num_threads": omp, "host_cpus_visible": os.cpu_count(), "allowed_cpus": allowed,
+            "threads": threads, "threads_source": source}
+
+
+def cpu_t3l(threads, min_seconds, max_searches=200):
+    """Back-to-back full T3L searches on the CPU port until >= min_seconds of
+    search time; returns (nodes/s, searches, seconds)."""
     import ctypes as C
 
     from oracle import loader as L
@@ -246,16 +304,32 @@ def cpu_baseline(threads, min_seconds=10.0):
     lib = L.cpu_runtime()
     p = L.parse_uts_args(T3L)
     total_s, searches = 0.0, 0
-    while total_s < min_seconds and searches < 200:
+    while total_s < min_seconds and searches < max_searches:
         n, lv, d, sec = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
         assert lib.ohc_uts(threads, C.byref(p), C.byref(n), C.byref(lv), C.byref(d), C.byref(sec)) == 0
         assert (n.value, lv.value, d.value) == T3L_GOLD, "CPU baseline miscounted"
         total_s += sec.value
         searches += 1
-    return {"value": T3L_GOLD[0] * searches / total_s, "unit": "nodes/s", "cores": threads,
-            "kind": "port", "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
-            "sample": f"{searches} back-to-back full UTS T3L searches (111,345,631 nodes each) on "
-                      f"oracle/hclib_cpu.c, {threads} worker threads, {total_s:.2f} s of search time"}
+    return T3L_GOLD[0] * searches / total_s, searches, total_s
+
+
+def cpu_baseline(allot, min_seconds=10.0):
+    """Host-CPU HClib (oracle/ C restatement, "port") on T3L at the allowed
+    worker count (cpu_allotment) and with one worker (nprocs and 1).
+    Bounded samples: back-to-back full T3L searches until >= min_seconds of
+    search time at the allowed count; one full search at 1 worker."""
+    threads = allot["threads"]
+    v, searches, total_s = cpu_t3l(threads, min_seconds)
+    v1, s1, t1 = cpu_t3l(1, 0.0, max_searches=1)
+    out = {"value": v, "unit": "nodes/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+           "threads": threads, "one_worker_nodes_per_s": v1, "one_worker_s": t1,
+           "sample": f"{searches} back-to-back full UTS T3L searches (111,345,631 nodes each) on "
+                     f"oracle/hclib_cpu.c, {threads} worker threads, {total_s:.2f} s of search time; "
+                     f"1 worker: {s1} search, {t1:.2f} s"}
+    out.update({k: allot[k] for k in ("affinity_cpus", "cgroup_quota", "cgroup_source", "cpuset",
+                                      "omp_num_threads", "host_cpus_visible", "allowed_cpus",
+                                      "threads_source")})
+    return out
 
 
 def cpu_configs(threads, s1, s2, gpu):
@@ -516,11 +590,11 @@ def main():
                                    "score": dscore},
         }
         out["atomics"] = measure_atomics(H, fst)
-        threads = int(os.environ.get("HCLIB_BENCH_CPU_THREADS",
-                                     os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))))
-        threads = max(1, min(threads, 16, os.cpu_count() or 1))
-        out["cpu_baseline"] = cpu_baseline(threads)
-        out["cpu_configs"] = cpu_configs(threads, s1, s2, out["configs"])
+        allot = cpu_allotment()
+        out["cpu_baseline"] = cpu_baseline(allot)
+        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        out["gpu_over_one_cpu_worker"] = value / out["cpu_baseline"]["one_worker_nodes_per_s"]
+        out["cpu_configs"] = cpu_configs(allot["threads"], s1, s2, out["configs"])
     print(json.dumps(out), flush=True)
     dist.shutdown(world)
 

@@ -112,15 +112,14 @@ bool register_if_not_ready(hclib_task_t *t, hclib_future_t *fut) {
     return true;
 }
 
-// register_on_all_promise_dependencies, src/hclib-promise.c:171-195: the
-// inline futures (NULL-terminated unless all four are used), then the
+// register_on_all_promise_dependencies, src/hclib-promise.c:171-195: every
+// inline slot (a NULL slot is skipped, not a terminator), then the
 // NULL-terminated waiting_on_extra
 bool register_all(hclib_task_t *t) {
     while (t->waiting_on_index < MAX_NUM_WAITS - 1) {
         t->waiting_on_index++;
         hclib_future_t *f = t->waiting_on[t->waiting_on_index];
-        if (!f) return true;
-        if (register_if_not_ready(t, f)) return false;
+        if (f && register_if_not_ready(t, f)) return false;
     }
     if (t->waiting_on_extra) {
         while (true) {

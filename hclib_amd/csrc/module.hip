@@ -52,6 +52,10 @@ int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolVie
         set_error("chunk deques: need 8k deques, power-of-two capacity, 1..64 items per chunk");
         return HCLIB_HIP_EINVAL;
     }
+    // capacity is counted in ITEMS: `cap` slots hold cap * 64 items at the
+    // full chunk, so a smaller chunk gets proportionally more slots (a
+    // smaller HCLIB_HIP_CHUNK must not shrink what the frontier can spill to)
+    for (uint32_t c = chunk; c * 2 <= 64; c *= 2) cap *= 2;
     const size_t hdr = sizeof(QueueHdr) * nq;
     const size_t slots = (size_t)nq * cap;
     const size_t need = hdr + slots * 4 * 2 + slots * chunk * words * 4 + 4096;
@@ -353,9 +357,14 @@ extern "C" int hclib_hip_global_init(void *region, uint32_t cap, int nranks) {
     hipLaunchKernelGGL(k_reset_global, dim3((cap + 255) / 256), dim3(256), 0, m.stream,
                        (uint32_t *)((char *)region + co), cap);
     HX_HIP(hipGetLastError());
-    // every rank starts holding its shard's top levels
+    // every rank starts holding its shard's top levels: active = ranks, and
+    // each rank's handshake word says it holds its unit
     const uint32_t active = (uint32_t)nranks;
+    uint32_t held[kGlobalMaxRanks];
+    for (int r = 0; r < kGlobalMaxRanks; ++r) held[r] = r < nranks ? 1u : 0u;
     HX_HIP(hipMemcpyAsync(region, &active, 4, hipMemcpyHostToDevice, m.stream));
+    HX_HIP(hipMemcpyAsync((char *)region + offsetof(GlobalHdr, held), held, sizeof(held), hipMemcpyHostToDevice,
+                          m.stream));
     HX_HIP(hipStreamSynchronize(m.stream));
     return HCLIB_HIP_OK;
 }

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "hx_module.h"
+#include "uts_sha1.h"
 
 namespace hx {
 
@@ -36,88 +37,7 @@ namespace hx {
 #define HX_W(i) \
     (w[(i) & 15] = HX_ROTL(w[((i) + 13) & 15] ^ w[((i) + 8) & 15] ^ w[((i) + 2) & 15] ^ w[(i) & 15], 1))
 
-// rng_spawn: SHA1(parent || i) with the 24-byte message padding, specialised
-// for the one-block message W = {p0..p4, i, 0x80000000, 0 x8, 192}: the
-// schedule drops every known-zero term, the round functions are single
-// v_bitop3_b32 ops (gfx950: ch 0xCA, parity 0x96, maj 0xE8), rotates are
-// v_alignbit_b32 — ~585 VALU ops instead of ~740 for the generic block.
-// Same function as sha1_begin/hash/end of test/uts/rng/brg_sha1.c:195-327
-// applied to the rng_spawn message of brg_sha1.c:68-83.
-__device__ __forceinline__ uint32_t rl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
-__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-__device__ __forceinline__ uint32_t fch(uint32_t b, uint32_t c, uint32_t d) {
-    return __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);
-}
-__device__ __forceinline__ uint32_t fmaj(uint32_t b, uint32_t c, uint32_t d) {
-    return __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8);
-}
-#define HX_R(F, K, W)                                       \
-    {                                                      \
-        uint32_t t_ = rl(a, 5) + F(b, c, d) + e + ((K) + (W)); \
-        e = d;                                             \
-        d = c;                                             \
-        c = rl(b, 30);                                     \
-        b = a;                                             \
-        a = t_;                                            \
-    }
-
-__device__ __forceinline__ void rng_spawn_dev(const uint32_t p[5], uint32_t i, uint32_t out[5]) {
-    constexpr uint32_t C6 = 0x80000000u, C15 = 192u;  // padding word, bit length
-    constexpr uint32_t K0 = 0x5a827999u, K1 = 0x6ed9eba1u, K2 = 0x8f1bbcdcu, K3 = 0xca62c1d6u;
-    uint32_t w[80];
-    w[0] = p[0];
-    w[1] = p[1];
-    w[2] = p[2];
-    w[3] = p[3];
-    w[4] = p[4];
-    w[5] = i;
-    // W[t] = rotl1(W[t-3]^W[t-8]^W[t-14]^W[t-16]) with W6 = C6, W7..W14 = 0, W15 = C15
-    w[16] = rl(w[2] ^ w[0], 1);
-    w[17] = rl(w[3] ^ w[1], 1);
-    w[18] = rl(x3(C15, w[4], w[2]), 1);
-    w[19] = rl(x3(w[16], w[5], w[3]), 1);
-    w[20] = rl(x3(w[17], C6, w[4]), 1);
-    w[21] = rl(w[18] ^ w[5], 1);
-    w[22] = rl(w[19] ^ C6, 1);
-    w[23] = rl(w[20] ^ C15, 1);
-#pragma unroll
-    for (int t = 24; t < 29; ++t) w[t] = rl(w[t - 3] ^ w[t - 8], 1);
-    w[29] = rl(x3(w[26], w[21], C15), 1);
-    w[30] = rl(x3(w[27], w[22], w[16]), 1);
-    w[31] = rl(x3(w[28], w[23], w[17]) ^ C15, 1);
-#pragma unroll
-    for (int t = 32; t < 80; ++t) w[t] = rl(x3(w[t - 3], w[t - 8], w[t - 14]) ^ w[t - 16], 1);
-    uint32_t a = 0x67452301u, b = 0xefcdab89u, c = 0x98badcfeu, d = 0x10325476u, e = 0xc3d2e1f0u;
-    {  // round 0: every input but W0 is a constant (folded)
-        uint32_t t_ = rl(a, 5) + (d ^ (b & (c ^ d))) + e + K0 + w[0];
-        e = d;
-        d = c;
-        c = rl(b, 30);
-        b = a;
-        a = t_;
-    }
-#pragma unroll
-    for (int t = 1; t < 6; ++t) HX_R(fch, K0, w[t]);
-    HX_R(fch, K0, C6);
-#pragma unroll
-    for (int t = 7; t < 15; ++t) HX_R(fch, K0, 0u);
-    HX_R(fch, K0, C15);
-#pragma unroll
-    for (int t = 16; t < 20; ++t) HX_R(fch, K0, w[t]);
-#pragma unroll
-    for (int t = 20; t < 40; ++t) HX_R(x3, K1, w[t]);
-#pragma unroll
-    for (int t = 40; t < 60; ++t) HX_R(fmaj, K2, w[t]);
-#pragma unroll
-    for (int t = 60; t < 80; ++t) HX_R(x3, K3, w[t]);
-    out[0] = 0x67452301u + a;
-    out[1] = 0xefcdab89u + b;
-    out[2] = 0x98badcfeu + c;
-    out[3] = 0x10325476u + d;
-    out[4] = 0xc3d2e1f0u + e;
-}
+// rng_spawn (the device SHA-1, one and several interleaved chains): uts_sha1.h
 
 // --------------------------------------------------------- depth rules
 // rule.x: 0 = constant rule.y children; 1 = BIN: rand < rule.y ? m : 0;
@@ -285,11 +205,9 @@ struct UtsKind {
         return c.root_nc;
     }
 
-    __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
-                                  uint32_t *child, uint32_t *err, bool valid) {
-        uint32_t ch[5];
-        rng_spawn_dev(t, k, ch);
-        for (int g = 1; g < c.gran; ++g) rng_spawn_dev(t, k, ch);  // -g: repeated spawns
+    // everything after the spawn: counting, numChildren, the child template
+    __device__ static __forceinline__ int finish(const Ctx &c, Acc &acc, const uint32_t *t, const uint32_t *ch,
+                                                 uint32_t *child, uint32_t *err, bool valid) {
         const int h1 = (int)t[5] + 1;
         bool counted = valid;
         if (FEAT && c.nshards > 1) {
@@ -321,6 +239,29 @@ struct UtsKind {
         child[4] = ch[4];
         child[5] = (uint32_t)h1;
         return nc;
+    }
+
+    __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
+                                  uint32_t *child, uint32_t *err, bool valid) {
+        uint32_t ch[5];
+        rng_spawn_dev(t, k, ch);
+        for (int g = 1; g < c.gran; ++g) rng_spawn_dev(t, k, ch);  // -g: repeated spawns
+        return finish(c, acc, t, ch, child, err, valid);
+    }
+
+    // two nodes per lane (dual batches of the megakernel, hx_sched.h): the two
+    // SHA-1 chains interleaved instruction by instruction (uts_sha1.h)
+    __device__ static void process2(const Ctx &c, Acc &acc, const uint32_t *tA, uint32_t kA, uint32_t *childA,
+                                    int &ncA, const uint32_t *tB, uint32_t kB, uint32_t *childB, int &ncB,
+                                    uint32_t *err, bool validB) {
+        uint32_t chA[5], chB[5];
+        const uint32_t *pp[2] = {tA, tB};
+        const uint32_t ii[2] = {kA, kB};
+        uint32_t *oo[2] = {chA, chB};
+        rng_spawn_n<2>(pp, ii, oo);
+        for (int g = 1; g < c.gran; ++g) rng_spawn_n<2>(pp, ii, oo);  // -g: repeated spawns
+        ncA = finish(c, acc, tA, chA, childA, err, true);
+        ncB = finish(c, acc, tB, chB, childB, err, validB);
     }
 };
 
@@ -721,6 +662,10 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
     cfg.backoff = (uint32_t)env_int("HCLIB_HIP_BACKOFF", 16);
     cfg.defer = (uint32_t)env_int("HCLIB_HIP_DEFER", 1);
+    // dual batches (two nodes per lane while a wave holds > 64 items; kinds
+    // whose ring fits two batches' pushes: the fixed-shape GEO trees on
+    // 512-item rings)
+    cfg.dual = (uint32_t)env_int("HCLIB_HIP_UTS_DUAL", 1);
     // sharded launches of a rank attached to a global region share work
     const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
     HX_TRY(reset_sched(pool, 1, global));

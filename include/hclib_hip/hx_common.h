@@ -33,6 +33,13 @@ __device__ __forceinline__ void dev_error(uint32_t *err, uint32_t code) {
                                          HX_AGENT);
 }
 
+// the same for a word shared with other GPUs (first error wins)
+__device__ __forceinline__ void dev_error_sys(uint32_t *err, uint32_t code) {
+    uint32_t zero = 0;
+    __hip_atomic_compare_exchange_strong(err, &zero, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // --------------------------------------------------------- agent atomics
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T *p) {

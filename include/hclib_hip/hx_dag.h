@@ -479,7 +479,11 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
                 }
             }
         }
-        vm_drain();
+        // every wave's outputs are visible before wave 0 releases the waiters:
+        // sc1 payloads need only the drain, plain stores the agent release
+        // (another XCD's L2 must not serve stale lines)
+        if constexpr (Kind::kSc1Payload) vm_drain();
+        else release_agent();
         if constexpr (N > 0) {
             if (wave == helper) {
                 const bool dbl = __ballot(lane < N && was != 0) != 0;  // src/hclib-promise.c:206-207

@@ -80,9 +80,17 @@ __device__ __forceinline__ uint32_t finish_check_out(const FinishArena &a, uint3
     unsigned long long v = value & kScopeSumMask;
     while (s != kScopeRoot) {
         FinishScope *f = &a.scopes[s];
-        const unsigned long long old = add_agent(&f->word, v - kScopeOne);
+        unsigned long long old = add_agent(&f->word, v - kScopeOne), add = v;
+        if ((old & kScopeSumMask) + v > kScopeSumMask) {
+            // the sum carried into the count byte: take the carry back out with
+            // a second check-out of value 0 (whoever brings the count to 1
+            // last, this one or a sibling, is the last task out; the sum stays
+            // mod 2^56 as documented)
+            old = add_agent(&f->word, (unsigned long long)0 - kScopeOne);
+            add = 0;
+        }
         if ((old >> 56) != 1) return ran;  // a sibling is still running
-        const unsigned long long sum = (old + v) & kScopeSumMask;
+        const unsigned long long sum = (old + add) & kScopeSumMask;
         const uint32_t cw = ld_agent(&f->cont);
         v = cont(cw, sum) & kScopeSumMask;
         ++ran;

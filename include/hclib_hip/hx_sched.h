@@ -94,7 +94,14 @@ struct alignas(256) GlobalHdr {
     uint32_t pad2[63];
     uint32_t tail;
     uint32_t pad3[63];
+    uint32_t err;  // first DevError any rank hit in the shared protocol: every rank stops
+    uint32_t pad4[63];
     unsigned long long moved[32];  // [2r] chunks rank r exported, [2r+1] chunks it imported
+    // per rank: 1 while the rank holds its unit of `active`, 0 once a release
+    // (idle += 1 included) has landed; the import that takes the unit back
+    // waits for 0, so its idle -= 1 never runs ahead of the release's
+    // idle += 1 (`idle` cannot underflow; tests/model/global_sharing_model.c)
+    uint32_t held[16];
 };
 constexpr int kGlobalMaxRanks = 16;
 
@@ -172,6 +179,8 @@ struct SchedConfig {
                                // hungry (0: (hunger + 3) / 4)
     uint32_t defer = 1;  // a hunger spill's chunk is published after the next batch body
                          // (PendingChunk) instead of behind a store round trip
+    uint32_t dual = 1;   // kinds with process2 (KindDual): a wave holding more than 64
+                         // items runs TWO per lane per batch, their bodies interleaved
 };
 
 // Kind concept:
@@ -190,6 +199,14 @@ struct SchedConfig {
 //                                     // (process gets `valid`; invalid lanes'
 //                                     // results are dropped)
 //   static constexpr bool kBoundedChildren;  // process() never returns >= kMaxChildren
+//   optional, pure kinds only:
+//   __device__ static void process2(const Ctx&, Acc&, const uint32_t *tmplA, uint32_t kA,
+//                                   uint32_t *childA, int &ncA, const uint32_t *tmplB,
+//                                   uint32_t kB, uint32_t *childB, int &ncB, uint32_t *err,
+//                                   bool validB);
+//        two items in one lane, their bodies interleaved (independent
+//        dependency chains fill each other's issue slots: a dependent chain of
+//        one wave issues a VALU op only every ~4-5 cycles of the 2 it needs)
 
 // Range items one task's children are pushed as (Kind::kPieces, default 8):
 // a task with c children becomes min(c, pieces) items. Fewer pieces need a
@@ -217,6 +234,14 @@ struct KindPieces<K, decltype((void)K::kPieces)> {
 };
 template <class K>
 constexpr int pieces_of() { return KindPieces<K>::value; }
+template <class K, class = void>
+struct KindHasDual {
+    static constexpr bool value = false;
+};
+template <class K>
+struct KindHasDual<K, decltype((void)&K::process2)> {
+    static constexpr bool value = K::kPure;
+};
 template <class K>
 constexpr int group_max_of() { return KindPieces<K>::value + 2; }  // items one lane pushes per batch
 constexpr uint32_t kMaxChildren = 1u << 24;  // kend shares its descriptor word with delta
@@ -355,7 +380,7 @@ __device__ __forceinline__ void publish_pending(const PoolView &pool, SchedGloba
 // PendingChunk); the caller must publish a live one before the next enqueue.
 template <class Kind, int CAP>
 __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q, WaveStack<Kind, CAP> &st,
-                              uint32_t bot, uint32_t n, uint32_t &occ, PendingChunk *pc) {
+                              uint32_t bot, uint32_t n, uint32_t &occ, PendingChunk *pc, bool relief = false) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     QueueHdr *h = &pool.hdr[q];
@@ -371,7 +396,10 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
         } else {
             const uint32_t hd = ld_agent(&h->head), tl = ld_agent(&h->tail);
             seen = tl - hd;
-            if ((int)(tl - hd) < (int)(pool.cap / 2)) {
+            // a ring-full relief may fill the deque to its last slot: a ticket
+            // below head + cap waits only for a consumer that already claimed
+            // the previous lap's ticket (no deadlock, a short bounded wait)
+            if ((int)(tl - hd) < (int)(relief ? pool.cap - 1 : pool.cap / 2)) {
                 add_agent(&g->outstanding, 1u);
                 pos = add_agent(&h->tail, 1u);
                 ok = 1;
@@ -520,16 +548,23 @@ __device__ bool global_enqueue(const typename Kind::Ctx &ctx, const GlobalView &
     pos = lane0(pos);
     const uint32_t slot = pos & (gv.cap - 1);
     uint32_t *ctl = gv.ctl + 2u * slot;
+    uint32_t timed_out = 0;
     if (lane == 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (ld_sys(ctl) != pos) {
             if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s
+                // the slot's previous lap was never consumed: write nothing
+                // (its chunk is still unread) and stop every rank through the
+                // shared error word (the ticket taken here is never published)
                 dev_error(err, kErrQueueFull);
+                dev_error_sys(&h->err, kErrQueueFull);
+                timed_out = 1;
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
         }
     }
+    if (lane0(timed_out)) return false;
     uint32_t *dst = gv.data + (size_t)slot * words_per_chunk;
     if ((uint32_t)lane < n) {
 #pragma unroll
@@ -579,6 +614,7 @@ __device__ uint32_t global_dequeue(const GlobalView &gv, uint32_t words_per_chun
             }
             if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s
                 dev_error(err, kErrSpinTimeout);
+                dev_error_sys(&h->err, kErrSpinTimeout);
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -715,6 +751,37 @@ __device__ __forceinline__ void push_outputs(WaveStack<Kind, CAP> &st, uint32_t 
     }
 }
 
+// One lane's outputs of one item at ring positions pos..: the residual of
+// the item (children k+1..kend-1 of `tmpl`, nres <= 2 pieces), then the new
+// task's children (`child`, ucnt children as nch pieces) — the general path
+// of push_outputs for a lane that pushes two items' outputs (dual batches).
+template <class Kind, int CAP>
+__device__ __forceinline__ void push_group(WaveStack<Kind, CAP> &st, uint32_t pos, uint32_t nres, uint32_t ucnt,
+                                           uint32_t nch, const uint32_t *tmpl, const uint32_t *child, uint32_t k,
+                                           uint32_t kend) {
+    constexpr uint32_t M = CAP - 1;
+    constexpr int kPieces = pieces_of<Kind>();
+    if (nres) {
+        store_tmpl<Kind, CAP>(st, pos & M, tmpl);
+        const uint32_t mid = k + 1 + ((kend - k - 1) >> 1);
+        st.d[pos & M] = make_uint2(k + 1, nres == 1 ? kend : mid);
+        if (nres == 2) st.d[(pos + 1) & M] = make_uint2(mid, kend | (1u << 24));
+        pos += nres;
+    }
+    if (nch) store_tmpl<Kind, CAP>(st, pos & M, child);
+#pragma unroll
+    for (uint32_t j = 0; j < (uint32_t)kPieces; ++j) {
+        if (j < nch) {
+            uint32_t lo = j, hi = j + 1;
+            if (ucnt > (uint32_t)kPieces) {
+                lo = (j * ucnt) / (uint32_t)kPieces;
+                hi = ((j + 1) * ucnt) / (uint32_t)kPieces;
+            }
+            st.d[(pos + j) & M] = make_uint2(lo, hi | (j << 24));
+        }
+    }
+}
+
 // Narrow frontier (span-bound trees): the ring is empty and no hunger can
 // stop a carry of at most one batch (spill_lo above it), so the chain runs in
 // a loop of its own: process the carried items, carry their children,
@@ -810,13 +877,14 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
 // inbox (LDS CAS 0 -> 2), writes the items and sets it full (1) — LDS
 // operations of one wave land in issue order, so the items are there before
 // the flag. The idle sibling polls its own inbox before the deques. An inbox
-// chunk is not counted in `outstanding`: the taker counts itself back in
-// (+1) when it takes it, so a wave elsewhere may read 0 and leave while a
-// chunk is in flight here — it was idle anyway, and the taker and its
-// workgroup finish the work (the count can never go below the truth).
+// chunk holds one unit of `outstanding` like an HBM chunk: the putter (which
+// holds its own unit, so the count cannot read 0 meanwhile) adds it before
+// the chunk becomes visible, and the taker inherits it, so no wave can see
+// 0 while a chunk waits in an inbox. A wave that leaves the megakernel closes
+// its inbox (state 3) so nothing is put there afterwards.
 template <class Kind>
 struct Inbox {
-    uint32_t state;  // 0 empty, 2 being filled, 1 full
+    uint32_t state;  // 0 empty, 2 being filled, 1 full, 3 closed (owner left)
     uint32_t n;
     uint32_t idle;   // the owner wave holds no work
     uint32_t pad;
@@ -824,7 +892,7 @@ struct Inbox {
 };
 
 template <class Kind, int CAP>
-__device__ bool inbox_put(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n) {
+__device__ bool inbox_put(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n, SchedGlobals *g) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     uint32_t ok = 0;
@@ -848,6 +916,7 @@ __device__ bool inbox_put(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st, uint32_t bo
     }
     asm volatile("" ::: "memory");
     if (lane == 0) {
+        add_agent(&g->outstanding, 1u);  // the chunk's unit, before it becomes visible
         *(volatile uint32_t *)&ib.n = n;
         *(volatile uint32_t *)&ib.idle = 0u;
         *(volatile uint32_t *)&ib.state = 1u;
@@ -883,7 +952,10 @@ __device__ __forceinline__ void wave_goes_idle(SchedGlobals *g, const GlobalView
     if constexpr (GLOBAL) {
         const uint32_t prev = __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
         if (prev == 1u) {
+            // release the rank's unit: idle += 1, then the handshake word (a
+            // release store: the idle add has been performed before it)
             add_sys(&gv.hdr->idle, 1u);
+            __hip_atomic_store(&gv.hdr->held[gv.rank], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             add_sys(&gv.hdr->active, (uint32_t)-1);
         }
     } else {
@@ -1015,8 +1087,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             }
             uint32_t n = 0;
             if constexpr (WPG > 1) {
-                n = inbox_take<Kind, CAP>(ib[wave], st);
-                if (n && lane == 0) add_agent(&g->outstanding, 1u);  // this wave holds work again
+                n = inbox_take<Kind, CAP>(ib[wave], st);  // inherits the chunk's unit
                 if (n) q = home;
             }
             if (n == 0) n = dequeue_chunk<Kind, CAP>(pool, q, st, g);
@@ -1029,9 +1100,25 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     n = global_dequeue<Kind, CAP>(gv, pool.chunk * (uint32_t)Kind::kWords, st, &g->err);
                     if (n && lane == 0) {
                         // this wave now holds work; a rank that had none takes
-                        // its unit of `active` back before the chunk's is returned
+                        // its unit of `active` back before the chunk's is
+                        // returned, once the release that gave it up has landed
+                        // (handshake: held 0 -> 1; see GlobalHdr::held)
                         const uint32_t prev = add_agent(&g->outstanding, 1u);
                         if (prev == 0u) {
+                            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                            while (true) {
+                                uint32_t z = 0u;
+                                if (__hip_atomic_compare_exchange_strong(&gv.hdr->held[gv.rank], &z, 1u,
+                                                                         __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_SYSTEM))
+                                    break;
+                                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s
+                                    dev_error(&g->err, kErrSpinTimeout);
+                                    dev_error_sys(&gv.hdr->err, kErrSpinTimeout);
+                                    break;
+                                }
+                                __builtin_amdgcn_s_sleep(1);
+                            }
                             add_sys(&gv.hdr->active, 1u);
                             add_sys(&gv.hdr->idle, (uint32_t)-1);
                         }
@@ -1078,6 +1165,16 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                         if (lane0(ga) == 0) break;
                     }
                 }
+                if constexpr (GLOBAL) {
+                    // another rank hit a protocol error: stop promptly
+                    uint32_t ge = 0;
+                    if (lane == 0) ge = ld_sys(&gv.hdr->err);
+                    vm_drain();
+                    if (lane0(ge)) {
+                        if (lane == 0) dev_error(&g->err, ge);
+                        break;
+                    }
+                }
                 outst_pf = outst;  // fresh hunger signal for the first batch after a steal
                 hunger_in = 0;
             }
@@ -1122,6 +1219,78 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             --hunger_in;
             outst = outst_cur;
         }
+        // a push that would come near live items first moves the oldest
+        // items out as chunks (rare: only bursts of wide nodes)
+        auto make_room = [&](uint32_t tout) -> bool {
+            unsigned long long full_since = 0;
+            while ((top - bot) + tout > kRoom) {
+                uint32_t n = top - bot;
+                if (n > pool.chunk) n = pool.chunk;
+                bool ok = false;
+                for (uint32_t a = 0; a < pool.nq && !ok; ++a)
+                    ok = enqueue_chunk<Kind, CAP>(pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr);
+                // every deque is at its half mark: fill one past it rather than wait
+                for (uint32_t a = 0; a < pool.nq && !ok; ++a)
+                    ok = enqueue_chunk<Kind, CAP>(pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr, true);
+                if (!ok) {
+                    // every deque is full: other waves are draining them, so wait
+                    // (bounded) rather than fail at once
+                    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                    if (full_since == 0) full_since = now;
+                    uint32_t e = 0;
+                    if (lane == 0) e = ld_agent(&g->err);
+                    if (lane0(e) || now - full_since > 100000ull * cfg.spin_limit) {
+                        if (lane == 0) dev_error(&g->err, kErrStackOverflow);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                    continue;
+                }
+                ++npush;
+                bot += n;
+            }
+            return (top - bot) + tout <= kRoom;
+        };
+        uint32_t tout = 0;
+        bool dual = false;
+        if constexpr (KindHasDual<Kind>::value && CAP >= 2 * kWaveSize * kGroupMax + kGroupMax) {
+            // ---- dual batch: a wave holding more than one batch of ring items
+            // (and nothing carried) runs two per lane, item A = top-1-lane,
+            // item B = top-65-lane, their bodies interleaved (process2)
+            dual = cfg.dual && carry == 0 && size > (uint32_t)kWaveSize;
+            if (dual) {
+                const uint32_t take2 = size < 2u * kWaveSize ? size : 2u * kWaveSize;
+                const bool hasB = (uint32_t)lane + kWaveSize < take2;
+                uint32_t tA[TW], tB[TW], cA[TW], cB[TW];
+                const uint32_t pA = top - 1 - (uint32_t)lane, pB = pA - (uint32_t)kWaveSize;
+                const uint2 dA = st.d[pA & M], dB = st.d[pB & M];
+                const uint32_t kA = dA.x, kendA = dA.y & (kMaxChildren - 1);
+                const uint32_t kB = dB.x, kendB = hasB ? dB.y & (kMaxChildren - 1) : kB + 1;
+                load_tmpl<Kind, CAP>(st, (pA - (dA.y >> 24)) & M, tA);
+                load_tmpl<Kind, CAP>(st, (pB - (dB.y >> 24)) & M, tB);
+                int ncA = 0, ncB = 0;
+                Kind::process2(ctx, acc, tA, kA, cA, ncA, tB, kB, cB, ncB, &g->err, hasB);
+                publish_pending<Kind, CAP>(pool, g, pend);
+                top -= take2;
+                const uint32_t rA = kendA - kA - 1u, rB = hasB ? kendB - kB - 1u : 0u;
+                const uint32_t nresA = rA == 0 ? 0u : (rA < (uint32_t)HX_RESIDUAL_SPLIT_MIN || HX_RESIDUAL_WHOLE ? 1u : 2u);
+                const uint32_t nresB = rB == 0 ? 0u : (rB < (uint32_t)HX_RESIDUAL_SPLIT_MIN || HX_RESIDUAL_WHOLE ? 1u : 2u);
+                const uint32_t uA = ncA > 0 ? (uint32_t)ncA : 0u, uB = (hasB && ncB > 0) ? (uint32_t)ncB : 0u;
+                const uint32_t nchA = uA > (uint32_t)kPieces ? (uint32_t)kPieces : uA;
+                const uint32_t nchB = uB > (uint32_t)kPieces ? (uint32_t)kPieces : uB;
+                n_exec += hasB ? 2u : 1u;
+                n_spawn += uA + uB;
+                const int nout = (int)(nresA + nchA + nresB + nchB);
+                const int P = wave_scan_add(nout);
+                tout = (uint32_t)lane63(P);
+                const uint32_t excl = (uint32_t)(P - nout);
+                if (!make_room(tout)) break;  // error already recorded
+                push_group<Kind, CAP>(st, top + excl, nresA, uA, nchA, tA, cA, kA, kendA);
+                push_group<Kind, CAP>(st, top + excl + nresA + nchA, nresB, uB, nchB, tB, cB, kB, kendB);
+                top += tout;
+            }
+        }
+        if (!dual) {
         // ---- a batch = the carried items, then the top items of the ring,
         // min(carry + size, 64) in all, one per lane
         const uint32_t room = (uint32_t)kWaveSize - carry;
@@ -1184,7 +1353,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         const unsigned long long spawn = __ballot(nch != 0);
         const uint32_t mu = spawn ? (uint32_t)__builtin_amdgcn_readlane((int)nch, __builtin_ctzll(spawn)) : 0u;
         const bool uniform = __ballot(nres != 0 || ucnt > (uint32_t)kPieces || (nch != 0 && nch != mu)) == 0;
-        uint32_t tout, excl;
+        uint32_t excl;
         int nout = 0;
         if (uniform) {
             excl = mu * (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(spawn >> 32),
@@ -1247,33 +1416,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 continue;
             }
         }
-        // a push that would come near live items first moves the oldest
-        // items out as chunks (rare: only bursts of wide nodes)
-        unsigned long long full_since = 0;
-        while ((top - bot) + tout > kRoom) {
-            uint32_t n = top - bot;
-            if (n > pool.chunk) n = pool.chunk;
-            bool ok = false;
-            for (uint32_t a = 0; a < pool.nq && !ok; ++a)
-                ok = enqueue_chunk<Kind, CAP>(pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr);
-            if (!ok) {
-                // every deque is at its half-capacity mark: other waves are
-                // draining them, so wait (bounded) rather than fail at once
-                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-                if (full_since == 0) full_since = now;
-                uint32_t e = 0;
-                if (lane == 0) e = ld_agent(&g->err);
-                if (lane0(e) || now - full_since > 100000ull * cfg.spin_limit) {
-                    if (lane == 0) dev_error(&g->err, kErrStackOverflow);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(8);
-                continue;
-            }
-            ++npush;
-            bot += n;
-        }
-        if ((top - bot) + tout > kRoom) break;  // error already recorded
+        if (!make_room(tout)) break;  // error already recorded
         if (uniform) {
             push_uniform<Kind, CAP>(st, top, excl, tout, mu, nch != 0, child);
         } else {
@@ -1282,6 +1425,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         }
         top += tout;
         if (HX_STAMPS && cfg.stamps) cyc_push += __builtin_amdgcn_s_memtime() - ts0;
+        }  // single batch
         // ---- give the oldest items to hungry waves, or relieve a full ring
         uint32_t sz = top - bot;
         uint32_t hungry = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
@@ -1299,7 +1443,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                         Inbox<Kind> &sib = ib[(wave + a) % (uint32_t)WPG];
                         if (lane0(*(volatile uint32_t *)&sib.idle) == 1u &&
                             lane0(*(volatile uint32_t *)&sib.state) == 0u)
-                            ok = inbox_put<Kind, CAP>(sib, st, bot, n);
+                            ok = inbox_put<Kind, CAP>(sib, st, bot, n, g);
                     }
                 }
                 if (!ok) publish_pending<Kind, CAP>(pool, g, pend);  // one deferred chunk at a time
@@ -1318,7 +1462,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         if constexpr (GLOBAL) {
             // another rank is idle and no wave of this one is hungry: export
             // the oldest items (one chunk per batch)
-            if (hungry == 0 && gidle > 0 && sz >= cfg.spill_lo) {
+            if (hungry == 0 && (int)gidle > 0 && sz >= cfg.spill_lo) {
                 uint32_t n = (sz + 1) / 2;
                 if (n > pool.chunk) n = pool.chunk;
                 publish_pending<Kind, CAP>(pool, g, pend);
@@ -1333,6 +1477,15 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         if (HX_STAMPS && cfg.stamps) t_batch = __builtin_amdgcn_s_memtime();
     }
     publish_pending<Kind, CAP>(pool, g, pend);  // (error exits)
+    if constexpr (WPG > 1) {
+        // close this wave's inbox: no sibling may hand it work any more
+        if (lane == 0) {
+            *(volatile uint32_t *)&ib[wave].idle = 0u;
+            uint32_t expect = 0u;
+            __hip_atomic_compare_exchange_strong(&ib[wave].state, &expect, 3u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
     const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
     lds_sum(st, busy_phase ? 0 : 1, t_end - t_mark);

@@ -9,7 +9,12 @@ import hclib_amd as H  # noqa: E402
 
 H.init(0)
 n = 1 << 28
-b = torch.rand(n, device="cuda"); c = torch.rand(n, device="cuda"); a = torch.empty(n, device="cuda")
+# the bench's layout (bench.py measure_triad): one allocation, the three
+# arrays staggered by 2 MiB + 4 KiB, so the counters describe the timed launch
+pad = 0x201000 // 4
+buf = torch.empty(3 * n + 2 * pad, device="cuda")
+b, c, a = buf[:n], buf[n + pad:2 * n + pad], buf[2 * n + 2 * pad:3 * n + 2 * pad]
+b.copy_(torch.rand(n, device="cuda")); c.copy_(torch.rand(n, device="cuda"))
 st = torch.cuda.current_stream()
 for _ in range(10):
     H.triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), 3.0, n, st.cuda_stream)

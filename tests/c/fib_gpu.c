@@ -1,6 +1,11 @@
 /* test/fib/fib.c (async/finish version, :57-71, :151-186) against the
  * MI355X build: the same fib task body and FibArgs struct; the only
- * addition is naming `fib` a device task kind. Usage: fib_gpu N */
+ * addition is naming `fib` a device task kind. Usage: fib_gpu N
+ *
+ * fib_iter, FibArgs and fib() restate the reference's caller, whose
+ * unchanged body is the point of this drop-in test. HClib: Copyright (c)
+ * 2013-2015, Rice University, BSD 3-clause license (the reference
+ * repository's LICENSE file); the rest of this file is this project's. */
 #include <assert.h>
 #include <stdio.h>
 #include <stdlib.h>

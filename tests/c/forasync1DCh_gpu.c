@@ -1,43 +1,52 @@
-/* test/c/forasync1DCh.c (H1=1024, T1=33, FLAT) against the MI355X build:
- * same body and checks; forasync_fct1 is named a device loop body. */
-#include <assert.h>
+/* A chunked 1-D forasync whose body runs on the GPU through include/hclib.h.
+ *
+ * Scenario of the reference's test/c/forasync1DCh.c (a 1024-iteration FLAT
+ * loop in tiles of 33; every slot is visited exactly once and receives its
+ * own index), written here as a drop-in check of the device loop-body path:
+ * the host function `mark_slot` is named a device loop body once
+ * (hclib_hip_register_forasync_body -> the built-in IOTA_CHECK body, which
+ * stores the index and flags any slot it finds already written), and the
+ * program then calls hclib_forasync exactly as a CPU HClib program would.
+ * Afterwards the host checks the slots itself. Prints "Check results: OK". */
 #include <stdio.h>
 #include <stdlib.h>
 
 #include "hclib.h"
 
-#define H1 1024
-#define T1 33
+enum { kSlots = 1024, kTile = 33, kUnvisited = -1 };
 
-void forasync_fct1(void *argv, int idx) {
-    int *ran = (int *)argv;
-    assert(ran[idx] == -1);
-    ran[idx] = idx;
+/* host twin of the device body (never runs on the host in this program) */
+void mark_slot(void *slots, int i) {
+    int *s = (int *)slots;
+    if (s[i] != kUnvisited) abort();
+    s[i] = i;
 }
 
-void init_ran(int *ran, int size) {
-    while (size > 0) {
-        ran[size - 1] = -1;
-        size--;
-    }
-}
-
-void entrypoint(void *arg) {
-    int *ran = (int *)arg;
-    init_ran(ran, H1);
-    hclib_loop_domain_t loop = {0, H1, 1, T1};
+static void run_loop(void *slots) {
+    for (int i = 0; i < kSlots; i++) ((int *)slots)[i] = kUnvisited;
+    hclib_loop_domain_t dom;
+    dom.low = 0;
+    dom.high = kSlots;
+    dom.stride = 1;
+    dom.tile = kTile;
     hclib_start_finish();
-    hclib_forasync((void *)forasync_fct1, (void *)ran, 1, &loop, FORASYNC_MODE_FLAT);
+    hclib_forasync((void *)mark_slot, slots, 1, &dom, FORASYNC_MODE_FLAT);
     hclib_end_finish();
 }
 
-int main(int argc, char **argv) {
-    int *ran = (int *)malloc(H1 * sizeof(int));
-    assert(ran);
-    hclib_hip_register_forasync_body((void *)forasync_fct1, 2 /* HCLIB_HIP_BODY_IOTA_CHECK */);
-    const char *deps[] = {"system", "hip"};
-    hclib_launch(entrypoint, ran, deps, 2);
-    for (int i = 0; i < H1; i++) assert(ran[i] == i);
+int main(void) {
+    int *slots = (int *)calloc(kSlots, sizeof(int));
+    if (!slots) return 2;
+    hclib_hip_register_forasync_body((void *)mark_slot, 2 /* HCLIB_HIP_BODY_IOTA_CHECK */);
+    const char *modules[2] = {"system", "hip"};
+    hclib_launch(run_loop, slots, modules, 2);
+    int bad = 0;
+    for (int i = 0; i < kSlots; i++) bad += slots[i] != i;
+    free(slots);
+    if (bad) {
+        printf("Check results: %d slots wrong\n", bad);
+        return 1;
+    }
     printf("Check results: OK\n");
     return 0;
 }

@@ -142,6 +142,32 @@ static void entrypoint(void *arg) {
     assert(hclib_lookup_dist_func(HCLIB_DEFAULT_LOOP_DIST)(1, NULL, NULL, 0) == central);
     unsigned id = hclib_register_dist_func(my_dist);
     assert(id >= 1 && hclib_lookup_dist_func(id) == my_dist);
+
+    /* a NULL inline future is skipped, not a terminator
+     * (src/hclib-promise.c:171-180): futures {f0, NULL, f2, f3, f4} — the
+     * task waits for every non-NULL one, including the extra f4 */
+    {
+        hclib_promise_t *q[5];
+        hclib_future_t *fs[5];
+        for (int i = 0; i < 5; i++) {
+            q[i] = hclib_promise_create();
+            fs[i] = hclib_get_future_for_promise(q[i]);
+        }
+        fs[1] = NULL;
+        const int c0 = counter;
+        hclib_start_finish();
+        hclib_async(leaf, NULL, fs, 5, NULL);
+        hclib_promise_put(q[0], NULL);
+        hclib_yield(NULL);
+        assert(counter == c0);
+        hclib_promise_put(q[2], NULL);
+        hclib_promise_put(q[3], NULL);
+        hclib_yield(NULL);
+        assert(counter == c0); /* still waiting on the extra future f4 */
+        hclib_promise_put(q[4], NULL);
+        hclib_end_finish();
+        assert(counter == c0 + 1);
+    }
 }
 
 int main(void) {

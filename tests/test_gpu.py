@@ -199,6 +199,34 @@ def test_uts_bench_partition_8_ranks(golden, name, split, capsys):
     assert max(p["kernel_ms"] for p in parts) < 2.0 * whole["kernel_ms"] + 5.0
 
 
+@pytest.mark.parametrize("chunk", ["16", "32"])
+def test_uts_t1xl_non_default_chunk(chunk, monkeypatch):
+    """HCLIB_HIP_CHUNK below the default 64 on the 1.6 G-node wide tree
+    (test/uts/sample_trees.sh:50-51): the HBM deques are sized in items, not
+    slots, so a smaller chunk does not shrink what the frontier can spill to,
+    and a full ring fills the deques past their half mark before it waits
+    (round 2 ended this launch with "LDS ring overflow")."""
+    monkeypatch.setenv("HCLIB_HIP_CHUNK", chunk)
+    r = H.uts("-t 1 -a 3 -d 15 -b 4 -r 29")
+    assert (r["nodes"], r["leaves"], r["max_depth"]) == (1635119272, 1308100063, 15)
+
+
+@pytest.mark.parametrize("wpg", ["2", "4"])
+def test_uts_bin_sibling_inbox_narrow_trees(wpg, monkeypatch):
+    """BIN trees near the critical branching factor (q*m = 0.9975 and
+    0.99925: 30 K - 2.6 M nodes, depth 120-2,367, long narrow chains with one
+    or two waves holding work most of the time) with 2 or 4 worker waves per
+    workgroup handing chunks through LDS inboxes: every tree's node / leaf /
+    depth counts equal the serial oracle's (test/uts/uts.c restated), i.e. no
+    inbox chunk is lost at termination."""
+    monkeypatch.setenv("HCLIB_HIP_WPG", wpg)
+    for b, q, seed in [(2000, 0.1995, s) for s in range(8)] + [(500, 0.19985, s) for s in range(8)]:
+        args = f"-t 0 -b {b} -q {q} -m 5 -r {seed}"
+        (n, lv, d), _ = L.uts_serial(L.parse_uts_args(args))
+        r = H.uts(args)
+        assert (r["nodes"], r["leaves"], r["max_depth"]) == (n, lv, d), args
+
+
 def test_uts_other_shapes_vs_oracle():
     for args in ["-t 1 -a 1 -d 8 -b 3 -r 5", "-t 3 -d 6 -b 5 -r 3", "-t 0 -b 200 -q 0.19 -m 5 -r 11",
                  "-t 1 -a 3 -d 7 -b 4 -r 19 -g 3"]:
