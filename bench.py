@@ -304,7 +304,7 @@ def cpu_t3l(threads, min_seconds, max_searches=200):
     lib = L.cpu_runtime()
     p = L.parse_uts_args(T3L)
     total_s, searches = 0.0, 0
-    while total_s < min_seconds and searches < max_searches:
+    while searches == 0 or (total_s < min_seconds and searches < max_searches):
         n, lv, d, sec = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
         assert lib.ohc_uts(threads, C.byref(p), C.byref(n), C.byref(lv), C.byref(d), C.byref(sec)) == 0
         assert (n.value, lv.value, d.value) == T3L_GOLD, "CPU baseline miscounted"

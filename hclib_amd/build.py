@@ -100,11 +100,43 @@ def build(verbose: bool = True, variant: str = "") -> str:
     keep = set(objs)
     for f in os.listdir(out):
         p = os.path.join(out, f)
-        if (f.endswith(".o") and p not in keep) or f.startswith("libhclib_amd.so."):
+        if (f.endswith(".o") and p not in keep) or (f.startswith("libhclib_amd.so.") and not f.endswith(".stamp")):
             os.remove(p)
     if verbose:
         print("built", lib)
+    build_modules(out, lib, cflags, verbose)
     return lib
+
+
+MODULES = {"hip": "modules/hclib_hip_module.hip"}
+
+
+def build_modules(out: str, lib: str, cflags, verbose: bool = True) -> list:
+    """The plug-in modules (libhclib_<name>.so beside libhclib_amd.so, where
+    hclib_launch's dlopen of `deps` finds them; src/hclib-runtime.c:294-317):
+    "hip" registers the GPU locale type and its memory callbacks."""
+    built = []
+    for name, src in MODULES.items():
+        so = os.path.join(out, f"libhclib_{name}.so")
+        path = os.path.join(CSRC, src)
+        key = _hash([path] + _headers() + [lib], cflags)
+        stamp = so + ".stamp"
+        if not (os.path.exists(so) and os.path.exists(stamp) and open(stamp).read() == key):
+            cmd = [HIPCC] + cflags + ["-shared", "-x", "hip", path, "-o", so + ".tmp", "-L" + out, "-lhclib_amd",
+                                      "-Wl,-rpath,$ORIGIN"]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"module {name} failed:\n{r.stderr[-6000:]}")
+            os.replace(so + ".tmp", so)
+            with open(stamp, "w") as fh:
+                fh.write(key)
+        for f in os.listdir(out):  # offload-bundle leftovers of the link step
+            if f.startswith(f"libhclib_{name}.so.") and not f.endswith(".stamp"):
+                os.remove(os.path.join(out, f))
+        built.append(so)
+        if verbose:
+            print("built", so)
+    return built
 
 
 def build_tests(verbose: bool = True) -> list:

@@ -144,13 +144,14 @@ int check_hip(int rc, const char *what) {
 // an error, as one rank drives one GPU in the multi-GPU launch.
 void ensure_gpu(const char *who, int device = -1) {
     if (device < 0) device = hx::env_int("HCLIB_HIP_DEVICE", hx::env_int("LOCAL_RANK", 0));
-    if (!rt().hip) {
+    const int have = hclib_hip_device();  // bound by an earlier call or by the hip module's callbacks
+    if (have < 0) {
         if (hclib_hip_init(device) != HCLIB_HIP_OK)
             die("%s: the hip module could not bind a gfx950 device: %s", who, hclib_hip_last_error());
-        rt().hip = true;
-    } else if (hx::mod().device != device) {
-        die("%s: this process drives GPU %d; GPU %d needs a process of its own", who, hx::mod().device, device);
+    } else if (have != device) {
+        die("%s: this process drives GPU %d; GPU %d needs a process of its own", who, have, device);
     }
+    rt().hip = true;
 }
 
 // the device a task at `locale` runs on (-1: the process's default)
@@ -433,8 +434,6 @@ void hclib_init(const char **deps, int ndeps, const int instrument) {
     hxh::load_dependencies(deps, ndeps);
     hclib_call_module_pre_init_functions();
     hxh::bind_worker0();  // builds the graph, makes current_ws() answer here
-    for (int i = 0; i < ndeps; ++i)
-        if (!strcmp(deps[i], "hip") || !strcmp(deps[i], "gpu")) ensure_gpu("hclib_init");
     hclib_call_module_post_init_functions();
     R.launched = true;
     current_finish() = nullptr;
@@ -811,45 +810,6 @@ void host_free(void *p, hclib_locale_t *) { free(p); }
 void host_memset(void *p, int v, size_t n, hclib_locale_t *) { memset(p, v, n); }
 void host_copy(hclib_locale_t *, void *d, hclib_locale_t *, void *s, size_t n) { memcpy(d, s, n); }
 
-// "GPU" callbacks: the MI355X counterpart of modules/cuda/src/hclib_cuda.cpp:69-139,
-// on the module's stream, each completed before its task returns
-hipStream_t gpu_stream(const char *who) {
-    ensure_gpu(who);
-    return hx::mod().stream;
-}
-void *gpu_alloc(size_t n, hclib_locale_t *) {
-    gpu_stream("hclib_allocate_at");
-    void *p = nullptr;
-    if (hipMalloc(&p, n ? n : 1) != hipSuccess) die("hclib_allocate_at: hipMalloc(%zu) failed", n);
-    return p;
-}
-void gpu_free(void *p, hclib_locale_t *) {
-    if (p && hipFree(p) != hipSuccess) die("hclib_free_at: hipFree failed");
-}
-void *gpu_realloc(void *p, size_t n, hclib_locale_t *l) {
-    void *q = gpu_alloc(n, l);
-    if (p) {
-        size_t old = 0;
-        if (hipMemPtrGetInfo(p, &old) != hipSuccess) die("hclib_reallocate_at: not a device allocation");
-        hipStream_t s = gpu_stream("hclib_reallocate_at");
-        if (hipMemcpyAsync(q, p, old < n ? old : n, hipMemcpyDeviceToDevice, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            die("hclib_reallocate_at: copy failed");
-        gpu_free(p, l);
-    }
-    return q;
-}
-void gpu_memset(void *p, int v, size_t n, hclib_locale_t *) {
-    hipStream_t s = gpu_stream("hclib_memset_at");
-    if (hipMemsetAsync(p, v, n, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-        die("hclib_memset_at: hipMemsetAsync failed");
-}
-void gpu_copy(hclib_locale_t *, void *d, hclib_locale_t *, void *src, size_t n) {
-    hipStream_t s = gpu_stream("hclib_async_copy");
-    if (hipMemcpyAsync(d, src, n, hipMemcpyDefault, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-        die("hclib_async_copy: hipMemcpyAsync(%zu bytes) failed", n);
-}
-
 Runtime::MemFuncs &mem_of(int type) {
     Runtime &R = rt();
     if (!R.mem_builtins) {
@@ -861,13 +821,9 @@ Runtime::MemFuncs &mem_of(int type) {
         h.memset = host_memset;
         h.copy = host_copy;
         h.copy_priority = MAY_USE;
-        Runtime::MemFuncs &g = R.mem[1];
-        g.alloc = gpu_alloc;
-        g.realloc = gpu_realloc;
-        g.free = gpu_free;
-        g.memset = gpu_memset;
-        g.copy = gpu_copy;
-        g.copy_priority = MUST_USE;  // modules/cuda/src/hclib_cuda.cpp:173
+        // a GPU locale type's callbacks come from the hip plug-in module
+        // (hclib_amd/csrc/modules/hclib_hip_module.hip), registered in its
+        // post-init like the reference's modules/cuda
     }
     return R.mem[type];
 }
@@ -1055,6 +1011,11 @@ loop_dist_func hclib_lookup_dist_func(unsigned id) {
 
 // the GPU locale standing for HIP device `index` (the first one of the graph)
 hclib_locale_t *hclib_hip_gpu_locale(int index) {
+    // asking for a GPU locale means using it: a host without a gfx950 device
+    // (or without the hip module loaded) fails here, loudly
+    if (hxh::gpu_type() == ~0u)
+        die("hclib_hip_gpu_locale: no GPU locale type (load the \"hip\" module: deps {\"system\", \"hip\"})");
+    ensure_gpu("hclib_hip_gpu_locale", index);
     const int n = hclib_get_num_locales();
     for (int i = 0; i < n; ++i) {
         hclib_locale_t *l = hclib_get_locale(i);

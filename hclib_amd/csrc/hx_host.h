@@ -10,13 +10,16 @@ namespace hxh {
 [[noreturn]] void die(const char *fmt, ...);
 
 // ---- modules (src/hclib_module.c:49-160, src/hclib-runtime.c:294-317)
-// dlopen libhclib_<dep>.so for each dep that is not built in ("hip"); the
-// library's HCLIB_REGISTER_MODULE runs in its static initialiser
+// dlopen libhclib_<dep>.so for each dep ("hip" is this project's
+// libhclib_hip.so plug-in, hclib_amd/csrc/modules/); the library's
+// HCLIB_REGISTER_MODULE runs in its static initialiser
 void load_dependencies(const char **deps, int ndeps);
 
 // ---- locale types and the graph (src/hclib-locality-graph.c)
 constexpr unsigned kSysmemType = 0;  // built in: system memory
-constexpr unsigned kGpuType = 1;     // built in: a GPU (modules/hip)
+// the "GPU" locale type once a module (modules/hip) has registered it, else
+// an id no locale has
+unsigned gpu_type();
 // build the graph once the modules' pre-init functions have run
 // (HCLIB_LOCALITY_FILE or the default graph); idempotent
 void build_graph();

@@ -46,7 +46,7 @@ std::vector<ModuleFns> &modules() {
 
 // ------------------------------------------------------- locale types
 std::vector<std::string> &types() {
-    static std::vector<std::string> t{"sysmem", "GPU"};  // kSysmemType, kGpuType
+    static std::vector<std::string> t{"sysmem"};  // kSysmemType; "GPU" comes from modules/hip
     return t;
 }
 struct MetaFns {
@@ -132,7 +132,7 @@ void finalize_graph(std::vector<std::pair<int, int>> &edges) {
     // GPU locales -> devices: "GPU<k>" is device k, otherwise the ordinal
     int ordinal = 0;
     for (size_t i = 0; i < n; ++i) {
-        if (G.locales[i].type != kGpuType) continue;
+        if (G.locales[i].type != gpu_type()) continue;
         const char *s = G.locales[i].lbl + 3;
         if (G.device[i] < 0) G.device[i] = (*s && isdigit((unsigned char)*s)) ? atoi(s) : ordinal;
         ordinal++;
@@ -387,7 +387,7 @@ void build_default() {
     G.locales.reserve(4);
     const int sys = add_locale("sysmem");
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    if (gpu_type() != ~0u && hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
     if (ndev > 0) {
         const int dev = hx::env_int("HCLIB_HIP_DEVICE", hx::env_int("LOCAL_RANK", 0));
         const int g = add_locale("GPU" + std::to_string(dev));
@@ -407,14 +407,6 @@ void build_default() {
     G.pop[0].push_back(&G.locales[(size_t)sys]);
     G.steal[0].push_back(&G.locales[(size_t)sys]);
     finalize_graph(edges);
-}
-
-// metadata the built-in hip module attaches to GPU locales
-size_t gpu_meta_size() { return sizeof(hclib_hip_locale_metadata_t); }
-void gpu_meta_populate(hclib_locale_t *l) {
-    hclib_hip_locale_metadata_t *m = (hclib_hip_locale_metadata_t *)l->metadata;
-    const int k = locale_device(l);
-    m->device = k >= 0 ? k : 0;
 }
 
 }  // namespace
@@ -443,7 +435,6 @@ void load_dependencies(const char **deps, int ndeps) {
     }
     for (int i = 0; i < ndeps; ++i) {
         const std::string name = deps[i];
-        if (name == "hip" || name == "gpu") continue;  // built in (modules/hip)
         void *h = nullptr;
         std::string tried;
         for (const std::string &d : dirs) {
@@ -467,10 +458,6 @@ void prepare() {
     if (pthread_key_create(&ws_key, nullptr) != 0) die("cannot create ws_key");
     g_ws0.id = 0;
     g_ws0.nworkers = 1;
-    // the hip module's GPU locale metadata (its "pre-init" is built in),
-    // unless a module registered its own
-    if (meta_fns().size() <= kGpuType || !meta_fns()[kGpuType].size)
-        hclib_add_locale_metadata_functions((int)kGpuType, gpu_meta_size, gpu_meta_populate);
     done = true;
 }
 }  // namespace
@@ -485,10 +472,17 @@ void build_graph() {
 
 int locale_device(const hclib_locale_t *l) {
     Graph &G = graph();
-    if (!l || l->type != kGpuType) return -1;
+    if (!l || l->type != gpu_type()) return -1;
     const ptrdiff_t i = l - G.locales.data();
     if (i < 0 || (size_t)i >= G.locales.size()) return -1;
     return G.device[(size_t)i];
+}
+
+unsigned gpu_type() {
+    const std::vector<std::string> &t = types();
+    for (size_t i = 0; i < t.size(); ++i)
+        if (t[i] == "GPU") return (unsigned)i;
+    return ~0u;
 }
 
 hclib_worker_state *worker0() { return &g_ws0; }

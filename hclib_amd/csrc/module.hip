@@ -249,6 +249,10 @@ void hclib_hip_finalize(void) {
 
 int hclib_hip_num_cus(void) { return g_mod.inited ? g_mod.num_cus : 0; }
 
+int hclib_hip_device(void) { return g_mod.inited ? g_mod.device : -1; }
+
+void *hclib_hip_stream(void) { return g_mod.inited ? (void *)g_mod.stream : nullptr; }
+
 void hclib_hip_last_sched_counters(uint64_t out[16]) {
     for (int i = 0; i < 16; ++i) out[i] = g_mod.last_counters[i];
 }

@@ -16,8 +16,10 @@
  * $HCLIB_ROOT/lib/libhclib_<dep>.so for every name in `deps` (and
  * $HCLIB_MODULE_PATH/libhclib_<dep>.so first, when set); the library's
  * static initialiser runs HCLIB_REGISTER_MODULE. A missing library is a
- * warning, as in the reference. "hip" is built in: it binds the process's
- * gfx950 device (include/hclib_hip.h, modules/hip).
+ * warning, as in the reference. "hip" is this project's plug-in module
+ * libhclib_hip.so (hclib_amd/csrc/modules/hclib_hip_module.hip, built beside
+ * libhclib_amd.so): it registers the "GPU" locale type, its metadata and its
+ * memory callbacks through this ABI, as modules/cuda does in the reference.
  */
 #ifndef HCLIB_MODULE_H
 #define HCLIB_MODULE_H

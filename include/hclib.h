@@ -151,7 +151,7 @@ hclib_future_t *hclib_async_copy(hclib_locale_t *dst_locale, void *dst, hclib_lo
 #define HCLIB_HIP_KIND_FIB 1 /* fib(void*) of test/fib/fib.c:57-71; arg = {int n; long res;} */
 #define HCLIB_HIP_KIND_UTS 2 /* UTS search; arg = hclib_hip_uts_task_t below */
 
-/* the metadata the built-in hip module attaches to every GPU-type locale
+/* the metadata the hip plug-in module (libhclib_hip.so) attaches to every GPU-type locale
  * (hclib_add_locale_metadata_functions): the HIP device it stands for */
 typedef struct {
     int device;

@@ -62,6 +62,10 @@ void hclib_hip_finalize(void);
 const char *hclib_hip_last_error(void);
 /* Number of CUs / XCDs of the bound device (0 if none). */
 int hclib_hip_num_cus(void);
+/* the bound device (-1 before hclib_hip_init) and the module's HIP stream
+ * (NULL before): what the hip plug-in module's memory callbacks run on */
+int hclib_hip_device(void);
+void *hclib_hip_stream(void);
 /* Module version string, also proves the library loads without a GPU. */
 const char *hclib_hip_version(void);
 /* Scheduler counters of the last megakernel launch (HCLIB_STATS analogue,

@@ -7,21 +7,29 @@
  * reference's locality_graphs/davinci.json: 12 workers, two sockets of six
  * L2s, two GPUs, an interconnect). Its module registers the locale types a
  * system module and a communication module would (L2, L3, Interconnect);
- * GPU locales are the built-in hip module's, with metadata naming the HIP
- * device. Checks the graph, worker 0's paths ("L2_$(id / 6)_$(id % 6)"
+ * the GPU type comes from the hip plug-in module named in deps
+ * (libhclib_hip.so, as the reference's modules/cuda registers it), with
+ * metadata naming the HIP device. Checks the graph, worker 0's paths ("L2_$(id / 6)_$(id % 6)"
  * interpreted for id 0), the locality queries and breadth-first closest-
  * locale search (src/hclib-locality-graph.c:901-1165).
  * With argv[1] == "nointerconnect" the module does not register the
  * Interconnect type, and loading must fail like the reference's
- * ("Unknown locale type", exit 1).
+ * ("Unknown locale type", exit 1); with "nohip" deps omit "hip", so the
+ * file's GPU locales have no type (the same failure). With "gpu" the
+ * program also allocates, fills and copies memory at the file's GPU0
+ * locale and checks, through hclib_hip_module_counts (looked up in the
+ * loaded module), that every operation ran the module's callbacks.
  */
+#define _GNU_SOURCE /* RTLD_DEFAULT */
 #include <assert.h>
+#include <dlfcn.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "hclib.h"
 
-static int with_interconnect = 1;
+static int with_interconnect = 1, with_hip = 1, use_gpu = 0;
 static int l2, l3, ic;
 
 static void pre(void) {
@@ -95,11 +103,37 @@ static void entrypoint(void *arg) {
     hclib_future_wait(hclib_memset_at(p, 0, 64 * sizeof(int), by_label("sysmem")));
     assert(p[63] == 0);
     hclib_free_at(p, by_label("sysmem"));
+
+    if (use_gpu) {
+        /* memory at the file's GPU0 locale: the hip module's callbacks */
+        void (*counts)(unsigned long long *) =
+            (void (*)(unsigned long long *))dlsym(RTLD_DEFAULT, "hclib_hip_module_counts");
+        assert(counts);
+        unsigned long long c0[6], c1[6];
+        counts(c0);
+        assert(c0[5] == 2); /* the module populated both GPU locales' metadata */
+        hclib_locale_t *g0 = by_label("GPU0"), *host = by_label("sysmem");
+        const size_t N = 1 << 16;
+        unsigned char *d = (unsigned char *)hclib_future_wait(hclib_allocate_at(N, g0));
+        assert(d);
+        hclib_future_wait(hclib_memset_at(d, 0x3c, N, g0));
+        unsigned char *h = (unsigned char *)malloc(N);
+        hclib_future_wait(hclib_async_copy(host, h, g0, d, N, NULL, 0));
+        for (size_t i = 0; i < N; ++i) assert(h[i] == 0x3c);
+        hclib_free_at(d, g0);
+        free(h);
+        counts(c1);
+        assert(c1[0] == c0[0] + 1 && c1[3] == c0[3] + 1 && c1[4] == c0[4] + 1 && c1[2] == c0[2] + 1);
+        printf("hip module callbacks: alloc %llu, memset %llu, copy %llu, free %llu\n", c1[0], c1[3], c1[4], c1[2]);
+    }
 }
 
 int main(int argc, char **argv) {
     if (argc > 1 && strcmp(argv[1], "nointerconnect") == 0) with_interconnect = 0;
-    hclib_launch(entrypoint, NULL, NULL, 0);
+    if (argc > 1 && strcmp(argv[1], "nohip") == 0) with_hip = 0;
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0) use_gpu = 1;
+    const char *deps[] = {"hip"};
+    hclib_launch(entrypoint, NULL, deps, with_hip ? 1 : 0);
     printf("Check results: OK\n");
     return 0;
 }

@@ -7,7 +7,9 @@
  * including a copy whose source is a future
  * (HCLIB_ASYNC_COPY_USE_FUTURE_AS_SRC, src/hclib-mem.c:227-233).
  * Prints "Check results: OK". */
+#define _GNU_SOURCE /* RTLD_DEFAULT */
 #include <assert.h>
+#include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -39,6 +41,13 @@ static void body(void *arg) {
     hclib_free_at(p, host);
 
     if (use_gpu) {
+        /* every GPU-locale operation below runs the hip plug-in module's
+         * registered callbacks (libhclib_hip.so, loaded through deps) */
+        void (*counts)(unsigned long long *) =
+            (void (*)(unsigned long long *))dlsym(RTLD_DEFAULT, "hclib_hip_module_counts");
+        assert(counts);
+        unsigned long long c0[6], c1[6];
+        counts(c0);
         int n = 0;
         hclib_locale_t **gpus = hclib_get_all_locales_of_type(hclib_add_known_locale_type("GPU"), &n);
         assert(n >= 1 && gpus[0] == hclib_get_locale(1));
@@ -73,6 +82,12 @@ static void body(void *arg) {
         hclib_free_at(d, g);
         free(h);
         free(h2);
+        counts(c1);
+        /* 1 alloc, 1 realloc, 1 free, 1 memset, 5 copies */
+        assert(c1[0] - c0[0] == 1 && c1[1] - c0[1] == 1 && c1[2] - c0[2] == 1 && c1[3] - c0[3] == 1 &&
+               c1[4] - c0[4] == 5);
+        printf("hip module callbacks: alloc %llu, realloc %llu, free %llu, memset %llu, copy %llu\n", c1[0], c1[1],
+               c1[2], c1[3], c1[4]);
     }
     free(q);
 }

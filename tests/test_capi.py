@@ -54,12 +54,15 @@ def test_host_locale_memory_operations():
 
 @pytest.mark.gpu
 def test_gpu_locale_memory_operations():
-    """The same at the GPU locale: hipMalloc / hipMemsetAsync / hipMemcpyAsync
-    callbacks, host<->GPU round trip, realloc keeping the prefix, a copy whose
+    """The same at the GPU locale: the hip plug-in module's hipMalloc /
+    hipMemsetAsync / hipMemcpyAsync callbacks (registered in its post-init,
+    like modules/cuda/src/hclib_cuda.cpp:169-174), host<->GPU round trip, realloc keeping the prefix, a copy whose
     source is a future (HCLIB_ASYNC_COPY_USE_FUTURE_AS_SRC)."""
     r = _run(_build("mem_locale"), "gpu")
     assert r.returncode == 0, r.stderr
     assert "Check results: OK" in r.stdout
+    # every GPU-locale operation ran the hip plug-in module's callbacks
+    assert "hip module callbacks: alloc 1, realloc 1, free 1, memset 1, copy 5" in r.stdout
 
 
 def test_device_kinds_fail_loudly_without_gpu():

@@ -78,6 +78,39 @@ def test_locality_file_with_gpu_locales(tmp_path):
     assert "Worker 1\n  pop path: L2_0_1 L3_0 sysmem" in r.stderr
 
 
+def test_locality_file_gpu_type_comes_from_the_hip_module(tmp_path):
+    """Without "hip" in deps nothing registers the GPU locale type, so the
+    file's GPU locales are unknown, as in the reference without
+    modules/cuda (src/hclib-locality-graph.c:322-367)."""
+    exe = _build_c("locality_file", str(tmp_path))
+    f = os.path.join(GOLD, "locality", "davinci.json")
+    r = _run(exe, "nohip", env={"HCLIB_LOCALITY_FILE": f})
+    assert r.returncode == 1
+    assert 'Unknown locale type for locale "GPU0"' in r.stderr
+
+
+def test_hip_module_library_exports():
+    import ctypes
+
+    so = os.path.join(LIBDIR, "libhclib_hip.so")
+    assert os.path.exists(so)
+    lib = ctypes.CDLL(so)
+    for sym in ("hclib_hip_module_counts", "hclib_hip_module_gpu_type"):
+        assert hasattr(lib, sym), sym
+
+
+@pytest.mark.gpu
+def test_locality_file_gpu_locale_memory_through_the_module(tmp_path):
+    """hclib_allocate_at / memset_at / async_copy / free_at at the GPU0
+    locale that davinci.json declares, run by the hip plug-in module's
+    registered callbacks (asserted through its counters)."""
+    exe = _build_c("locality_file", str(tmp_path))
+    f = os.path.join(GOLD, "locality", "davinci.json")
+    r = _run(exe, "gpu", env={"HCLIB_LOCALITY_FILE": f})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Check results: OK" in r.stdout and "hip module callbacks: alloc 1" in r.stdout
+
+
 def test_locality_file_unknown_locale_type_is_fatal(tmp_path):
     exe = _build_c("locality_file", str(tmp_path))
     f = os.path.join(GOLD, "locality", "davinci.json")
