@@ -3,7 +3,7 @@
 # rocprofv3 kernel-trace (bench.json + kernel stats of the SAME command), the
 # triad PMC passes, the CPU-port thread sweep. Each GPU step has its own limit;
 # steps chained with &&. usage: scripts/gpu_r03.sh OUTDIR [steps...]
-# steps: ub ab tests bench pmc sweep (default: all)
+# steps: ub valu bands ab tests bench pmc sweep (default: all)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -14,6 +14,14 @@ has() { [[ " $STEPS " == *" $1 "* ]]; }
 if has ub; then
   timeout -k 10 120 scripts/ubench/ub_sha2.bin > $OUT/ub_sha2.log 2>&1 || { echo "ub failed"; exit 1; }
   cat $OUT/ub_sha2.log
+fi
+if has valu; then
+  timeout -k 10 120 scripts/ubench/ub_valu.bin > $OUT/ub_valu.log 2>&1 || { echo "valu failed"; exit 1; }
+  cat $OUT/ub_valu.log
+fi
+if has bands; then
+  timeout -k 10 300 python -u scripts/t3l_bands.py > $OUT/t3l_bands.jsonl 2> $OUT/t3l_bands.err || { echo "bands failed"; tail -20 $OUT/t3l_bands.err; exit 1; }
+  cat $OUT/t3l_bands.jsonl
 fi
 if has ab; then
   for T in T1XL T1L T1; do

@@ -1,0 +1,63 @@
+"""T3L per-depth-band table: for each band of depths,
+the tree's width there (nodes per level, from the kernel's own per-level
+histogram), and the leading edge's time per level from the diagnostic trace
+(HCLIB_HIP_UTS_TRACE=1: per depth the earliest 100 MHz stamp any wave
+reached it), in ns and in 2.4 GHz cycles, against the 2,636-cycle one-wave
+SHA-1 step (profiles/r02/ub_sha_split.log). Prints one JSON object per band
+and a summary line; `--bands N` sets the band width in levels."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+import hclib_amd as H  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--band", type=int, default=1000)
+ap.add_argument("--tree", default="-t 0 -b 2000 -q 0.200014 -m 5 -r 7")
+a = ap.parse_args()
+
+H.init(0)
+levels = 17845
+plain = [H.uts(a.tree, max_levels=levels) for _ in range(3)]
+width = np.array(plain[0]["levels"], dtype=np.int64)
+os.environ["HCLIB_HIP_UTS_TRACE"] = "1"
+r = H.uts(a.tree, max_levels=levels)
+del os.environ["HCLIB_HIP_UTS_TRACE"]
+t = np.array(r["levels"], dtype=np.float64)
+# depth 0 is not stamped (the root comes from roots(), which counts into
+# slot 0 instead): the leading edge starts at depth 1
+t[0] = t[1]
+ok = t < 2 ** 63
+depth = int(ok.sum())
+t = (t[:depth] - t[:depth].min()) * 10.0  # ns
+step = np.diff(t)  # step[d] = time from reaching depth d to depth d + 1
+ghz = 2.4
+print(json.dumps({"tree": a.tree, "plain_ms": [round(p["kernel_ms"], 3) for p in plain],
+                  "traced_ms": round(r["kernel_ms"], 3), "depths": depth,
+                  "edge_ms": round(t[-1] / 1e6, 3)}), flush=True)
+rows = []
+for d0 in range(0, depth - 1, a.band):
+    d1 = min(d0 + a.band, depth - 1)
+    s = step[d0:d1]
+    w = width[d0:d1]
+    rows.append({"depths": [d0, d1], "nodes_per_level_mean": round(float(w.mean()), 1),
+                 "nodes_per_level_max": int(w.max()), "ns_per_level": round(float(s.mean()), 1),
+                 "cycles_per_level": round(float(s.mean()) * ghz, 0),
+                 "excess_cycles_over_sha": round(float(s.mean()) * ghz - 2636, 0),
+                 "band_ms": round(float(s.sum()) / 1e6, 3),
+                 "levels_over_2x_sha": int((s * ghz > 2 * 2636).sum())})
+    print(json.dumps(rows[-1]), flush=True)
+# widths vs step time across all levels: where the excess lives
+tot_excess = sum(max(0.0, (q["cycles_per_level"] - 2636)) * (q["depths"][1] - q["depths"][0]) for q in rows)
+worst = max(rows, key=lambda q: q["excess_cycles_over_sha"] * (q["depths"][1] - q["depths"][0]))
+for lo, hi in [(0, 64), (64, 256), (256, 1024), (1024, 4096), (4096, 10 ** 9)]:
+    m = (width[:depth - 1] >= lo) & (width[:depth - 1] < hi)
+    if m.any():
+        print(json.dumps({"width": [lo, hi], "levels": int(m.sum()), "ns_per_level": round(float(step[m].mean()), 1),
+                          "ms": round(float(step[m].sum()) / 1e6, 3)}), flush=True)
+print(json.dumps({"summary": True, "excess_ms_total": round(tot_excess / ghz / 1e6, 3),
+                  "worst_band": worst["depths"]}), flush=True)
