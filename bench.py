@@ -563,6 +563,21 @@ def main():
             "bound": "span", "levels": T3L_GOLD[2],
             "ns_per_level": uts_ms * 1e6 / T3L_GOLD[2],
         }
+        if wide:
+            # the wide tree's kernel against its VALU ceiling: one rng_spawn
+            # SHA-1 per node is the unavoidable work, and the chip's rate of
+            # that exact instruction stream (measured here, every lane
+            # chaining spawns back to back) is the peak
+            cal = [(H.sha1_calibrate(ch, wpc, 2000)[0], ch, wpc) for ch, wpc in ((1, 12), (2, 12), (1, 16))]
+            peak, ch, wpc = max(cal)
+            ach = 1635119272 / (wide["kernel_ms_per_rank"][0] * 1e-3)
+            out["roofline_uts"] = {
+                "bound": "valu", "kernel": "k_uts_search (UTS T1XL, throughput-bound wide tree)",
+                "achieved": ach, "peak": peak, "unit": "nodes/s", "frac": ach / peak,
+                "peak_source": f"hclib_hip_sha1_calibrate: the rng_spawn SHA-1 of uts_sha1.h back to back, "
+                               f"best of {[(round(c[0] / 1e9, 1), c[1], c[2]) for c in cal]} "
+                               f"(G SHA-1/s, chains per lane, waves per CU)",
+            }
         t1 = min((H.uts(T1) for _ in range(3)), key=lambda r: r["kernel_ms"])
         assert (t1["nodes"], t1["leaves"], t1["max_depth"]) == T1_GOLD
         fv, fst = H.fib(30)

@@ -119,6 +119,8 @@ def lib():
                                             C.POINTER(C.c_uint64)]
         L.hclib_hip_atomic_calibrate.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double),
                                                  C.POINTER(C.c_double)]
+        L.hclib_hip_sha1_calibrate.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                               C.POINTER(C.c_double)]
         L.hclib_hip_global_bytes.restype = C.c_size_t
         L.hclib_hip_global_bytes.argtypes = [C.c_uint32]
         L.hclib_hip_global_init.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
@@ -332,6 +334,15 @@ def atomic_calibrate(mode: int, iters: int = 256):
     r, ms = C.c_double(), C.c_double()
     _check(lib().hclib_hip_atomic_calibrate(mode, iters, C.byref(r), C.byref(ms)),
            "hclib_hip_atomic_calibrate")
+    return r.value, ms.value
+
+
+def sha1_calibrate(chains: int = 1, waves_per_cu: int = 8, iters: int = 2000):
+    """The chip's UTS SHA-1 issue ceiling (SHA-1/s, kernel ms): the
+    rng_spawn stream of k_uts_search back to back on every lane."""
+    r, ms = C.c_double(), C.c_double()
+    _check(lib().hclib_hip_sha1_calibrate(chains, waves_per_cu, iters, C.byref(r), C.byref(ms)),
+           "hclib_hip_sha1_calibrate")
     return r.value, ms.value
 
 

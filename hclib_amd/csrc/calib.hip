@@ -20,6 +20,7 @@
 // Each mode is a plain kernel over a fixed number of operations; the rate is
 // ops / kernel time (HIP events on the module stream).
 #include "hx_module.h"
+#include "uts_sha1.h"
 
 namespace hx {
 
@@ -68,9 +69,78 @@ __global__ __launch_bounds__(256) void k_atomic_coalesced32(uint32_t *tab, uint3
     }
 }
 
+// The UTS rng_spawn SHA-1 (uts_sha1.h, the instruction stream k_uts_search
+// runs per node) back to back: every lane chains CH independent spawns
+// (state_{k+1} = SHA1(state_k || k)) for `iters` steps, WPC waves per CU.
+// The rate is the chip's SHA-1 issue ceiling: the "peak" of a kernel whose
+// unavoidable per-node work is one such compression (k_uts_search on a
+// throughput-bound tree; SURVEY §8d "Int VALU (SHA-1)").
+template <int CH>
+__global__ __launch_bounds__(64) void k_sha1_chain(const uint32_t *seed, int iters, uint32_t *sink) {
+    const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
+    uint32_t s[CH][5], o[CH][5];
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s[j][k] = seed[(gid * 5 + k) & 1023] ^ (0x9e3779b9u * (uint32_t)(j + 1));
+    for (int it = 0; it < iters; ++it) {
+        const uint32_t *pp[CH];
+        uint32_t ii[CH];
+        uint32_t *oo[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            pp[j] = s[j];
+            ii[j] = (uint32_t)it;
+            oo[j] = o[j];
+        }
+        rng_spawn_n<CH>(pp, ii, oo);
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) s[j][k] = o[j][k];
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) x ^= s[j][k];
+    if (x == 0x5eed5eedu) sink[0] = x;  // keeps the chains live
+}
+
 }  // namespace hx
 
 using namespace hx;
+
+extern "C" int hclib_hip_sha1_calibrate(int chains, int waves_per_cu, int iters, double *sha1_per_s,
+                                        double *kernel_ms) {
+    if (chains < 1 || chains > 2 || waves_per_cu < 1 || waves_per_cu > 16 || iters < 1 || iters > (1 << 16) ||
+        !sha1_per_s) {
+        set_error("hclib_hip_sha1_calibrate: chains 1..2, waves_per_cu 1..16, iters in [1, 2^16]");
+        return HCLIB_HIP_EINVAL;
+    }
+    HX_TRY(ensure_device());
+    Module &m = mod();
+    void *d = nullptr;
+    HX_HIP(hipMalloc(&d, 4096 + 256));
+    uint32_t *seed = (uint32_t *)d, *sink = (uint32_t *)((char *)d + 4096);
+    int rc = hip_check(hipMemsetAsync(d, 0x5a, 4096 + 256, m.stream), "memset");
+    const int blocks = m.num_cus * waves_per_cu;
+    for (int rep = 0; rep < 2 && rc == HCLIB_HIP_OK; ++rep) {  // warm-up, then the timed launch
+        if (rep == 1) rc = hip_check(hipEventRecord(m.ev0, m.stream), "event");
+        if (chains == 1) hipLaunchKernelGGL(k_sha1_chain<1>, dim3(blocks), dim3(64), 0, m.stream, seed, iters, sink);
+        else hipLaunchKernelGGL(k_sha1_chain<2>, dim3(blocks), dim3(64), 0, m.stream, seed, iters, sink);
+        if (rc == HCLIB_HIP_OK) rc = hip_check(hipGetLastError(), "sha1 calibration launch");
+    }
+    if (rc == HCLIB_HIP_OK) rc = hip_check(hipEventRecord(m.ev1, m.stream), "event");
+    if (rc == HCLIB_HIP_OK) rc = hip_check(hipStreamSynchronize(m.stream), "sync");
+    float ms = 0;
+    if (rc == HCLIB_HIP_OK) rc = hip_check(hipEventElapsedTime(&ms, m.ev0, m.ev1), "elapsed");
+    (void)hipFree(d);
+    if (rc != HCLIB_HIP_OK) return rc;
+    *sha1_per_s = ms > 0 ? (double)blocks * 64.0 * chains * iters / (ms * 1e-3) : 0.0;
+    if (kernel_ms) *kernel_ms = ms;
+    return HCLIB_HIP_OK;
+}
 
 extern "C" int hclib_hip_atomic_calibrate(int mode, int iters, double *mops_per_s, double *kernel_ms) {
     if (mode < 0 || mode > 2 || iters < kUnroll || iters > (1 << 20) || !mops_per_s) {

@@ -24,6 +24,7 @@ struct DagState {
     void *arena = nullptr;
     size_t arena_bytes = 0;
     uint32_t ntasks = 0, npromises = 0;
+    unsigned long long *trace = nullptr;  // HX_STAMPS builds: the per-task timeline
 };
 
 DagState g_dag;
@@ -138,6 +139,20 @@ extern "C" int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t
     v.ntasks = ntasks;
     v.npromises = npromises;
     v.payload_words = payload_words;
+    v.trace = nullptr;
+#if defined(HX_STAMPS) && HX_STAMPS
+    // diagnostic: per-task timeline (hx_dag.h kDagTraceWords), written to the
+    // file HCLIB_HIP_DAG_TRACE names at hclib_hip_dag_end
+    if (getenv("HCLIB_HIP_DAG_TRACE") && ntasks) {
+        if (g_dag.trace) (void)hipFree(g_dag.trace);
+        g_dag.trace = nullptr;
+        const size_t tb = (size_t)ntasks * kDagTraceWords * 8;
+        if (hipMalloc((void **)&g_dag.trace, tb) == hipSuccess) {
+            HX_HIP(hipMemsetAsync(g_dag.trace, 0, tb, m.stream));
+            v.trace = g_dag.trace;
+        }
+    }
+#endif
     v.spin_ms = spin_limit_ms ? spin_limit_ms : (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     g_dag.ntasks = ntasks;
     g_dag.npromises = npromises;
@@ -179,6 +194,14 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
 #if defined(HX_STAMPS) && HX_STAMPS
+    if (v.trace) {
+        std::vector<unsigned long long> tr((size_t)g_dag.ntasks * kDagTraceWords);
+        HX_HIP(hipMemcpy(tr.data(), v.trace, tr.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE *f = fopen(getenv("HCLIB_HIP_DAG_TRACE"), "wb")) {
+            fwrite(tr.data(), 8, tr.size(), f);
+            fclose(f);
+        }
+    }
     if (st[0] && (st[3] | st[4] | st[5]))
         fprintf(stderr, "dag group phases (cycles per task, wave 0): take %.0f body %.0f put %.0f\n",
                 (double)st[3] / st[0], (double)st[4] / st[0], (double)st[5] / st[0]);

@@ -109,6 +109,12 @@ void hclib_hip_last_narrow_counters(uint64_t out[4]);
 #define HCLIB_HIP_ATOMIC_HOT_WORD 1
 #define HCLIB_HIP_ATOMIC_COALESCED32 2
 int hclib_hip_atomic_calibrate(int mode, int iters, double *mops_per_s, double *kernel_ms);
+/* The chip's UTS SHA-1 issue ceiling: `chains` (1 or 2) independent rng_spawn
+ * chains per lane (the instruction stream k_uts_search runs per node),
+ * waves_per_cu waves on every CU, `iters` spawns per chain; SHA-1
+ * compressions per second over the timed launch (the peak of the UTS
+ * kernel's VALU roofline; bench.py `roofline_uts`). */
+int hclib_hip_sha1_calibrate(int chains, int waves_per_cu, int iters, double *sha1_per_s, double *kernel_ms);
 
 /* ----------------------------------------------- user device task kinds */
 /* The persistent-megakernel scheduler for task kinds compiled in the

@@ -50,7 +50,15 @@ struct DagView {
     uint32_t *err;               // DevError
     unsigned long long *stats;   // [0] tasks run, [1] puts, [2] releases
     uint32_t ntasks, npromises, payload_words, spin_ms;
+    // diagnostic build (HX_STAMPS) with HCLIB_HIP_DAG_TRACE set: per task
+    // kDagTraceWords 100 MHz stamps (see run_dag_group); null otherwise
+    unsigned long long *trace;
 };
+// trace record of task t: [0] released (its last counter decrement
+// returned), [1] started (the workgroup has its id), [2] body done (every
+// wave drained), [3] puts done, [4] 1 if its releaser kept it, [5] the
+// workgroup, [6] the task that released it
+constexpr int kDagTraceWords = 8;
 
 // Per-wave state a task body receives: the view and the wave's counters.
 struct DagWave {
@@ -421,6 +429,14 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
         if (t == kDagEmpty) break;
         if (!Kind::kSc1Payload) acquire_agent();
         stamp(0);
+#if defined(HX_STAMPS) && HX_STAMPS
+        if (view.trace && threadIdx.x == 0) {
+            unsigned long long *r = view.trace + (size_t)t * kDagTraceWords;
+            r[1] = __builtin_amdgcn_s_memrealtime();
+            r[4] = kept ? 1ull : 0ull;
+            r[5] = blockIdx.x;
+        }
+#endif
         if constexpr (N > 0) {
             if (wave == helper) {
                 // prefetch the waiter lists of the task's promises (the CSR is
@@ -492,6 +508,9 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
         }
         if (__syncthreads_or(!ok)) break;
         stamp(1);
+#if defined(HX_STAMPS) && HX_STAMPS
+        if (view.trace && threadIdx.x == 0) view.trace[(size_t)t * kDagTraceWords + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
         if constexpr (N > 0) {
             if (wave == 0) {
                 const uint32_t nwait = sh.nwait;
@@ -515,6 +534,12 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
                     if (!dbl && (uint32_t)lane < nwait) {
                         const uint32_t c = sh.waiter[lane];
                         if (add_agent(&view.deps[c], (uint32_t)-1) == 1u) rt = c;
+#if defined(HX_STAMPS) && HX_STAMPS
+                        if (view.trace && rt == c) {
+                            view.trace[(size_t)c * kDagTraceWords + 0] = __builtin_amdgcn_s_memrealtime();
+                            view.trace[(size_t)c * kDagTraceWords + 6] = t;
+                        }
+#endif
                     }
                     unsigned long long m = __ballot(rt != kDagEmpty);
                     uint32_t skip = 0;
@@ -548,6 +573,9 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
             }
         }
         stamp(2);
+#if defined(HX_STAMPS) && HX_STAMPS
+        if (view.trace && threadIdx.x == 0) view.trace[(size_t)t * kDagTraceWords + 3] = __builtin_amdgcn_s_memrealtime();
+#endif
         ++ran;
     }
     if (wave == 0 && lane == 0) {

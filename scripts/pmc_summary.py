@@ -11,14 +11,19 @@ for f in glob.glob(f"{root}/p*/p_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         if "uts" in r["Kernel_Name"]:
             d[r["Counter_Name"]] += float(r["Counter_Value"])
-nb = None
+nb = nn = None
 for f in glob.glob(f"{root}/p*.log"):
-    m = re.search(r"batches (\d+)", open(f).read())
+    t = open(f).read()
+    m = re.search(r"batches (\d+)", t)
     if m:
         nb = int(m.group(1))
-print(root, "batches", nb)
+    m = re.search(r"nodes (\d+)", t)
+    if m:
+        nn = int(m.group(1))
+print(root, "batches", nb, "nodes", nn)
 quad = {"SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
         "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_SCA", "SQ_WAIT_INST_LDS"}
 for k in sorted(d):
     v = d[k] * (4 if k in quad else 1)
-    print(f"  {k:24s} {v:16.0f}  per batch {v / nb:10.1f}" if nb else f"  {k} {v}")
+    per_node = f"  per 64 nodes {64 * v / nn:10.1f}" if nn else ""
+    print(f"  {k:24s} {v:16.0f}  per batch {v / nb:10.1f}{per_node}" if nb else f"  {k} {v}")
