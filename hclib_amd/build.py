@@ -35,7 +35,7 @@ CFLAGS = [
 ]
 
 
-VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "strict": ["-DHX_STRICT_HANDOFF=1"],
+VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "trace": ["-DHX_TRACE=1"], "strict": ["-DHX_STRICT_HANDOFF=1"],
             "narrow_noinline": ["-DHX_NARROW_NOINLINE=1"],
             "sched_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
             "sched_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],

@@ -24,7 +24,7 @@ struct DagState {
     void *arena = nullptr;
     size_t arena_bytes = 0;
     uint32_t ntasks = 0, npromises = 0;
-    unsigned long long *trace = nullptr;  // HX_STAMPS builds: the per-task timeline
+    unsigned long long *trace = nullptr;  // HX_DAG_TRACE builds: the per-task timeline
 };
 
 DagState g_dag;
@@ -140,7 +140,7 @@ extern "C" int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t
     v.npromises = npromises;
     v.payload_words = payload_words;
     v.trace = nullptr;
-#if defined(HX_STAMPS) && HX_STAMPS
+#if HX_DAG_TRACE
     // diagnostic: per-task timeline (hx_dag.h kDagTraceWords), written to the
     // file HCLIB_HIP_DAG_TRACE names at hclib_hip_dag_end
     if (getenv("HCLIB_HIP_DAG_TRACE") && ntasks) {
@@ -193,8 +193,9 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
     for (size_t p = 0; p < sat.size(); ++p) satisfied_out[p] = sat[p] ? 1 : 0;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
-#if defined(HX_STAMPS) && HX_STAMPS
+#if HX_DAG_TRACE
     if (v.trace) {
+        HX_HIP(hipStreamSynchronize(m.stream));
         std::vector<unsigned long long> tr((size_t)g_dag.ntasks * kDagTraceWords);
         HX_HIP(hipMemcpy(tr.data(), v.trace, tr.size() * 8, hipMemcpyDeviceToHost));
         if (FILE *f = fopen(getenv("HCLIB_HIP_DAG_TRACE"), "wb")) {
@@ -202,6 +203,8 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
             fclose(f);
         }
     }
+#endif
+#if defined(HX_STAMPS) && HX_STAMPS
     if (st[0] && (st[3] | st[4] | st[5]))
         fprintf(stderr, "dag group phases (cycles per task, wave 0): take %.0f body %.0f put %.0f\n",
                 (double)st[3] / st[0], (double)st[4] / st[0], (double)st[5] / st[0]);

@@ -59,6 +59,9 @@ struct SwCtx {
     int *right_out;      // [nth*th]
     int form;            // multi-wave bands: 100 * rows per lane + 10 * skew + hand-off steps / 16
     int bh;              // multi-wave band height (64 * rows per lane)
+    // diagnostic build (HX_STAMPS): the DAG's per-task trace (hx_dag.h
+    // kDagTraceWords), where tile tasks stamp their waves' phases; else null
+    unsigned long long *dtrace;
 };
 
 // alignment_score_matrix (smith_waterman.cpp:36-43) row for s2 code a, plus
@@ -755,6 +758,10 @@ struct SwBand {
     int *rightcol_lds;   // also keep the right column here
     int *corner_lds;     // H(R0, C0 + ncols): the right neighbour's corner
     int *corner_out_lds = nullptr;  // the bottom row's last value, also here
+    // diagnostic (HX_DAG_TRACE builds): the tile task's trace record, where
+    // waves 0 / 1 stamp their loop start ([12] / [15]) and wave 0 its first
+    // and third 64-step chunks ([13], [14]); null otherwise
+    unsigned long long *trec = nullptr;
 };
 
 // The workgroup's ingress wave: moves the top row into ring 0 and publishes
@@ -922,7 +929,14 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
     const int cofs = (S * lane) & 3;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = true;
+    auto trec = [&](int k) {
+        if (HX_DAG_TRACE && B.trec && lane == 0) B.trec[k] = __builtin_amdgcn_s_memrealtime();
+    };
+    if (w == 0) trec(12);
+    if (w == 1) trec(15);
     for (int s0 = 0; ok && s0 < ncols + D; s0 += 64) {
+        if (w == 0 && s0 == 64) trec(13);
+        if (w == 0 && s0 == 192) trec(14);
         const int slot = s0 & (kSwRing - 1);
         // ring_out's slots for columns s0 - D .. s0 + 63 - D are free
         if (s0 + 64 - D - kSwRing > 0 && !sw_band_spin(c, &cons[w + 1], s0 + 64 - D - kSwRing, t0)) {
@@ -1145,14 +1159,30 @@ struct SwDagWgKind {
         B.hout = c.bottom + (size_t)t * c.tw;
         B.corner_out = c.corner + t;
         B.corner_out_lds = last + 3;  // the corner promise's datum (datums())
+        B.trec = HX_DAG_TRACE && c.dtrace ? c.dtrace + (size_t)t * kDagTraceWords : nullptr;
         __syncthreads();  // every wave has read `last`
         if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod[0..63], cons[0..63]
         if (threadIdx.x == 0) *last = (int)t;
         __syncthreads();
         unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
-        if (wave == nw) return sw_band_ingress(c, B, rings, prod, cons);
-        if (wave == nw + 1) return sw_band_egress(c, B, rings + (size_t)nw * kSwRingStride, prod, cons);
+        // trace words 8.. (stamps build): [8] ingress done, [9] egress done,
+        // [10 + w] compute wave w done
+        auto tstamp = [&](int k) {
+            if (HX_DAG_TRACE && c.dtrace && lane_id() == 0)
+                c.dtrace[(size_t)t * kDagTraceWords + k] = __builtin_amdgcn_s_memrealtime();
+        };
+        if (wave == nw) {
+            const bool r = sw_band_ingress(c, B, rings, prod, cons);
+            tstamp(8);
+            return r;
+        }
+        if (wave == nw + 1) {
+            const bool r = sw_band_egress(c, B, rings + (size_t)nw * kSwRingStride, prod, cons);
+            tstamp(9);
+            return r;
+        }
         const bool ok = sw_band_row_any(c.form, c, B, wave, rings, dummy, code_rings, prod, cons, ph, false);
+        if (wave < 6) tstamp(10 + wave);
         if (HX_STAMPS && lane_id() == 0 && wave < 4)
             for (int q = 0; q < 6 && wave < 3; ++q) add_agent(&c.stats[4 + 6 * wave + q], ph[q]);
         return ok;
@@ -1274,6 +1304,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     c.left_in = nullptr;
     c.right_out = nullptr;
     c.progressive = env_int("HCLIB_HIP_SW_PROGRESSIVE", 1);
+    c.dtrace = nullptr;
     c.form = form;
     c.bh = bh;
     int rc = HCLIB_HIP_OK;
@@ -1331,6 +1362,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
             const size_t blds = sw_band_lds_bytes(th / bh) + (4 + 2 * (size_t)th) * 4;  // + kept right columns
             if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_wg,
                                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
+            c.dtrace = ((const DagView *)L.view)->trace;
             hipLaunchKernelGGL(k_sw_dag_wg, dim3(L.grid), dim3(64 * (th / bh) + 128), blds, m.stream, c,
                                *(const DagView *)L.view);
         } else {
@@ -1473,6 +1505,7 @@ extern "C" int hclib_hip_sw_band_begin(const int8_t *s1, size_t n1, const int8_t
     c.j0 = j0;
     c.j1 = j1;
     c.progressive = env_int("HCLIB_HIP_SW_PROGRESSIVE", 1);
+    c.dtrace = nullptr;
     c.form = sw_pick_form(th, 412);
     c.bh = sw_form_bh(c.form);
     c.spin_ms = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);

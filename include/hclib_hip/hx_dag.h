@@ -50,15 +50,22 @@ struct DagView {
     uint32_t *err;               // DevError
     unsigned long long *stats;   // [0] tasks run, [1] puts, [2] releases
     uint32_t ntasks, npromises, payload_words, spin_ms;
-    // diagnostic build (HX_STAMPS) with HCLIB_HIP_DAG_TRACE set: per task
+    // diagnostic builds (HX_STAMPS, HX_TRACE) with HCLIB_HIP_DAG_TRACE set: per task
     // kDagTraceWords 100 MHz stamps (see run_dag_group); null otherwise
     unsigned long long *trace;
 };
 // trace record of task t: [0] released (its last counter decrement
 // returned), [1] started (the workgroup has its id), [2] body done (every
 // wave drained), [3] puts done, [4] 1 if its releaser kept it, [5] the
-// workgroup, [6] the task that released it
-constexpr int kDagTraceWords = 8;
+// workgroup, [6] the task that released it; [8..15] the Kind's own stamps
+constexpr int kDagTraceWords = 16;
+// the per-task trace is compiled into the stamps build and into the lighter
+// trace build (HX_TRACE: these stamps only, none of the per-phase ones)
+#if (defined(HX_STAMPS) && HX_STAMPS) || (defined(HX_TRACE) && HX_TRACE)
+#define HX_DAG_TRACE 1
+#else
+#define HX_DAG_TRACE 0
+#endif
 
 // Per-wave state a task body receives: the view and the wave's counters.
 struct DagWave {
@@ -429,7 +436,7 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
         if (t == kDagEmpty) break;
         if (!Kind::kSc1Payload) acquire_agent();
         stamp(0);
-#if defined(HX_STAMPS) && HX_STAMPS
+#if HX_DAG_TRACE
         if (view.trace && threadIdx.x == 0) {
             unsigned long long *r = view.trace + (size_t)t * kDagTraceWords;
             r[1] = __builtin_amdgcn_s_memrealtime();
@@ -508,7 +515,7 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
         }
         if (__syncthreads_or(!ok)) break;
         stamp(1);
-#if defined(HX_STAMPS) && HX_STAMPS
+#if HX_DAG_TRACE
         if (view.trace && threadIdx.x == 0) view.trace[(size_t)t * kDagTraceWords + 2] = __builtin_amdgcn_s_memrealtime();
 #endif
         if constexpr (N > 0) {
@@ -534,7 +541,7 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
                     if (!dbl && (uint32_t)lane < nwait) {
                         const uint32_t c = sh.waiter[lane];
                         if (add_agent(&view.deps[c], (uint32_t)-1) == 1u) rt = c;
-#if defined(HX_STAMPS) && HX_STAMPS
+#if HX_DAG_TRACE
                         if (view.trace && rt == c) {
                             view.trace[(size_t)c * kDagTraceWords + 0] = __builtin_amdgcn_s_memrealtime();
                             view.trace[(size_t)c * kDagTraceWords + 6] = t;
@@ -573,7 +580,7 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
             }
         }
         stamp(2);
-#if defined(HX_STAMPS) && HX_STAMPS
+#if HX_DAG_TRACE
         if (view.trace && threadIdx.x == 0) view.trace[(size_t)t * kDagTraceWords + 3] = __builtin_amdgcn_s_memrealtime();
 #endif
         ++ran;

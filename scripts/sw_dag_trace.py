@@ -1,6 +1,7 @@
 """SW-64K promise DAG: one tile's timeline along the critical path (VERDICT r2
 item 7). Runs the reference's 3-promise tile program (HCLIB_HIP_SW_SCHED=dag)
-on the diagnostic build (HX_STAMPS: hclib_amd/lib/stamps/) with the per-task
+on the diagnostic build (HX_TRACE: hclib_amd/lib/trace/, these stamps
+only; HCLIB_AMD_LIB may name the heavier stamps build) with the per-task
 trace on (hx_dag.h kDagTraceWords: released / started / body done / puts
 done, kept, workgroup, releaser), then walks back from the last tile through
 the task whose put released each tile. Per hop it splits the time into
@@ -9,14 +10,14 @@ the task whose put released each tile. Per hop it splits the time into
   body:    started -> every wave of the tile drained
 and prints the totals by hop kind (row hop = left neighbour released it,
 column hop = up neighbour, diagonal). Build first:
-  python -m hclib_amd.build --variant stamps"""
+  python -m hclib_amd.build --variant trace"""
 import json
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("HCLIB_AMD_LIB", os.path.join(ROOT, "hclib_amd", "lib", "stamps", "libhclib_amd.so"))
+os.environ.setdefault("HCLIB_AMD_LIB", os.path.join(ROOT, "hclib_amd", "lib", "trace", "libhclib_amd.so"))
 out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "sw_dag_trace.bin")
 os.makedirs(os.path.dirname(out), exist_ok=True)
 os.environ["HCLIB_HIP_SW_SCHED"] = "dag"
@@ -35,7 +36,7 @@ score, st = H.sw(s1, s2, 256, 256)
 del os.environ["HCLIB_HIP_DAG_TRACE"]
 assert score == 128772
 ntw = nth = 256
-tr = np.fromfile(out, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+tr = np.fromfile(out, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
 assert tr.shape[0] == ntw * nth
 t0 = tr[0, 1]
 ns = lambda x: float(x) * 10.0  # 100 MHz ticks -> ns
@@ -48,7 +49,15 @@ while t != 0:
     kind = "row" if (ri, rj) == (i, j - 1) else "col" if (ri, rj) == (i - 1, j) else "diag"
     hops.append({"t": t, "kind": kind, "kept": int(tr[t, 4]),
                  "release": ns(tr[t, 0] - tr[r, 2]), "pickup": ns(tr[t, 1] - tr[t, 0]),
-                 "body": ns(tr[t, 2] - tr[t, 1]), "put": ns(tr[t, 3] - tr[t, 2])})
+                 "body": ns(tr[t, 2] - tr[t, 1]), "put": ns(tr[t, 3] - tr[t, 2]),
+                 # inside the body, from its start: ingress done, compute waves
+                 # 0 / 1 done, egress done (sw.hip SwDagWgKind stamps)
+                 "in_ingress": ns(tr[t, 8] - tr[t, 1]), "in_wave0": ns(tr[t, 10] - tr[t, 1]),
+                 "in_wave1": ns(tr[t, 11] - tr[t, 1]), "in_egress": ns(tr[t, 9] - tr[t, 1]),
+                 # wave 0's loop start, after its first chunk (steps 0-63) and
+                 # its third (steps 128-191); wave 1's loop start
+                 "in_w0_loop": ns(tr[t, 12] - tr[t, 1]), "in_w0_c1": ns(tr[t, 13] - tr[t, 1]),
+                 "in_w0_c3": ns(tr[t, 14] - tr[t, 1]), "in_w1_loop": ns(tr[t, 15] - tr[t, 1])})
     t = r
 hops.reverse()
 total = ns(tr[ntw * nth - 1, 2] - t0)
@@ -59,7 +68,8 @@ for kind in ("row", "col", "diag", "all"):
     if not hs:
         continue
     res[kind] = {"hops": len(hs), "kept": sum(h["kept"] for h in hs)}
-    for k in ("release", "pickup", "body", "put"):
+    for k in ("release", "pickup", "body", "put", "in_ingress", "in_w0_loop", "in_w0_c1", "in_w0_c3", "in_wave0",
+              "in_w1_loop", "in_wave1", "in_egress"):
         v = np.array([h[k] for h in hs])
         res[kind][k + "_us"] = round(float(v.mean()) / 1e3, 3)
         res[kind][k + "_ms_total"] = round(float(v.sum()) / 1e6, 3)
