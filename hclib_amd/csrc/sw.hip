@@ -87,6 +87,13 @@ __device__ __forceinline__ int shift_up1(int v) {
 #ifndef HX_STAMPS
 #define HX_STAMPS 0
 #endif
+// Timing experiments on the band sweep (diagnostic builds only, results are
+// wrong by design): 1 = lanes 0..62 skip their dummy ring writes (exec-masked
+// store by lane 63 alone), 2 = no top-ring loads (lane 0's up value is a
+// constant), 3 = no code loads (a constant score row)
+#ifndef HX_SW_EXP
+#define HX_SW_EXP 0
+#endif
 __device__ __forceinline__ unsigned long long sw_stamp() {
 #if HX_STAMPS
     unsigned long long t;
@@ -676,8 +683,9 @@ __device__ __forceinline__ void sw_band_subR(int s, int ncols, const int *top4, 
                                              const uint32_t (&mrow)[R], int (&lr)[R], int &diag) {
     constexpr int G = K / 4;
     const int lane = lane_id();
-    int4 tn = *(const int4 *)top4, tn2 = *(const int4 *)(top4 + 4);
-    uint32_t cn = code4[0], cn2 = code4[1];
+    int4 tn = HX_SW_EXP == 2 ? make_int4(s, s, s, s) : *(const int4 *)top4,
+         tn2 = HX_SW_EXP == 2 ? tn : *(const int4 *)(top4 + 4);
+    uint32_t cn = HX_SW_EXP == 3 ? 0x01020300u : code4[0], cn2 = HX_SW_EXP == 3 ? cn : code4[1];
 #pragma unroll
     for (int m = 0; m < G; ++m) {
         const int4 tc = tn;
@@ -685,8 +693,8 @@ __device__ __forceinline__ void sw_band_subR(int s, int ncols, const int *top4, 
         tn = tn2;
         cn = cn2;
         if (m + 2 < G) {
-            tn2 = *(const int4 *)(top4 + 4 * (m + 2));
-            cn2 = code4[m + 2];
+            if (HX_SW_EXP != 2) tn2 = *(const int4 *)(top4 + 4 * (m + 2));
+            if (HX_SW_EXP != 3) cn2 = code4[m + 2];
         }
         uint32_t sc[R];
 #pragma unroll
@@ -709,7 +717,7 @@ __device__ __forceinline__ void sw_band_subR(int s, int ncols, const int *top4, 
                 up = h;
             }
             diag = MASK ? (v ? up0 : diag) : up0;
-            wb[k] = lr[R - 1];
+            if (HX_SW_EXP != 1 || lane == 63) wb[k] = lr[R - 1];
         }
     }
 }
@@ -759,8 +767,7 @@ struct SwBand {
     int *corner_lds;     // H(R0, C0 + ncols): the right neighbour's corner
     int *corner_out_lds = nullptr;  // the bottom row's last value, also here
     // diagnostic (HX_DAG_TRACE builds): the tile task's trace record, where
-    // waves 0 / 1 stamp their loop start ([12] / [15]) and wave 0 its first
-    // and third 64-step chunks ([13], [14]); null otherwise
+    // waves 0 / 1 stamp their loop start ([12] / [15]); null otherwise
     unsigned long long *trec = nullptr;
 };
 
@@ -929,14 +936,10 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
     const int cofs = (S * lane) & 3;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = true;
-    auto trec = [&](int k) {
-        if (HX_DAG_TRACE && B.trec && lane == 0) B.trec[k] = __builtin_amdgcn_s_memrealtime();
-    };
-    if (w == 0) trec(12);
-    if (w == 1) trec(15);
+    // (trace builds: the loop start only — a stamp inside the loop, an SMEM
+    // read, waits for every LDS operation in flight and slows the sweep)
+    if (HX_DAG_TRACE && B.trec && lane == 0 && w < 2) B.trec[w == 0 ? 12 : 15] = __builtin_amdgcn_s_memrealtime();
     for (int s0 = 0; ok && s0 < ncols + D; s0 += 64) {
-        if (w == 0 && s0 == 64) trec(13);
-        if (w == 0 && s0 == 192) trec(14);
         const int slot = s0 & (kSwRing - 1);
         // ring_out's slots for columns s0 - D .. s0 + 63 - D are free
         if (s0 + 64 - D - kSwRing > 0 && !sw_band_spin(c, &cons[w + 1], s0 + 64 - D - kSwRing, t0)) {
@@ -1138,6 +1141,9 @@ struct SwDagWgKind {
         // parity) and its right neighbour's corner, for a row successor
         int *last = cons + 64, *corner_keep = last + 1, *right_keep = last + 4;  // [2][th]
         const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
+        // `last` (the workgroup's previous tile) and the zeroed prod / cons
+        // flags were written by after_body before the DAG's slot barrier:
+        // the body starts without a barrier of its own
         const bool from_lds = j > 0 && *last == (int)t - 1;
         SwBand B;
         B.R0 = i * c.th;
@@ -1160,10 +1166,6 @@ struct SwDagWgKind {
         B.corner_out = c.corner + t;
         B.corner_out_lds = last + 3;  // the corner promise's datum (datums())
         B.trec = HX_DAG_TRACE && c.dtrace ? c.dtrace + (size_t)t * kDagTraceWords : nullptr;
-        __syncthreads();  // every wave has read `last`
-        if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod[0..63], cons[0..63]
-        if (threadIdx.x == 0) *last = (int)t;
-        __syncthreads();
         unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
         // trace words 8.. (stamps build): [8] ingress done, [9] egress done,
         // [10 + w] compute wave w done
@@ -1186,6 +1188,19 @@ struct SwDagWgKind {
         if (HX_STAMPS && lane_id() == 0 && wave < 4)
             for (int q = 0; q < 6 && wave < 3; ++q) add_agent(&c.stats[4 + 6 * wave + q], ph[q]);
         return ok;
+    }
+    // between tiles (every wave done with this one): the hand-off flags back
+    // to 0 and this tile recorded as the workgroup's last, for the next body
+    __device__ static void after_body(const SwCtx &c, uint32_t t) {
+        extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+        int *prod = flags_of(c), *last = prod + 128;
+        if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod[0..63], cons[0..63]
+        if (threadIdx.x == 0) *last = (int)t;
+    }
+    __device__ static int *flags_of(const SwCtx &c) {
+        extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+        const int nw = c.th / c.bh;
+        return (int *)((uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * 128) + nw * 2048);
     }
     // right column, bottom row, corner (:212-226): run_dag_group's split put
     // (waiters prefetched while the tile runs, one release for all three)
@@ -1211,8 +1226,10 @@ __global__ __launch_bounds__(1024) void k_sw_dag_wg(SwCtx c, DagView v) {
     extern __shared__ __attribute__((aligned(16))) int sw_lds[];
     __shared__ uint32_t task_slot;
     const int nw = c.th / c.bh;
-    int *last = (int *)((uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * 128) + nw * 2048) + 128;
-    if (threadIdx.x == 0) *last = -2;  // no tile yet (run_dag_group's barriers order this)
+    int *prod = (int *)((uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * 128) + nw * 2048);
+    int *last = prod + 128;
+    if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod / cons (after_body resets them between tiles)
+    if (threadIdx.x == 0) *last = -2;  // no tile yet (run_dag_group's first barrier orders these)
     run_dag_group<SwDagWgKind>(c, v, &task_slot);
 }
 

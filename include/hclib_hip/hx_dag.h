@@ -27,6 +27,8 @@
 // acquires at agent scope before running a task it took from the list.
 #pragma once
 
+#include <type_traits>
+
 #include "hx_common.h"
 
 namespace hx {
@@ -328,6 +330,17 @@ struct group_put_n { static constexpr int value = 0; };
 template <class K>
 struct group_put_n<K, decltype((void)K::kPutN)> { static constexpr int value = K::kPutN; };
 
+// Optional: static void after_body(const Ctx&, uint32_t task), run by every
+// thread once every wave has finished the task's body (before its put).
+template <class K, class = void>
+struct has_after_body : std::false_type {};
+template <class K>
+struct has_after_body<K, decltype((void)&K::after_body)> : std::true_type {};
+template <class Kind>
+__device__ __forceinline__ void group_after_body(const typename Kind::Ctx &ctx, uint32_t t) {
+    if constexpr (has_after_body<Kind>::value) Kind::after_body(ctx, t);
+}
+
 // State the waves of one workgroup share across its tasks (LDS).
 struct DagGroupShared {
     uint32_t slot;        // the task wave 0 found
@@ -351,7 +364,7 @@ struct DagGroupShared {
 //     wave 0 decrements the waiters' counters, keeps one released task and
 //     leaves the others in LDS;
 //   * the last wave appends those (and the kept task's skip) to the ready
-//     list while wave 0 is already looking for the next task.
+//     list while the next task (the kept one) already runs.
 template <class Kind>
 __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view, uint32_t *slot_unused) {
     (void)slot_unused;
@@ -383,17 +396,6 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
         bool kept = false;
         uint32_t pend_pos = 0;
         int pend_lane = 0;
-        if (N > 0 && wave == helper) {
-            // the previous put's releases: one tail fetch-add for all of them
-            const uint32_t np = sh.npend, sk = sh.skip;
-            if (np + sk) {
-                uint32_t base = 0;
-                if (lane == 0) base = add_agent(view.tail, np + sk);
-                base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
-                if ((uint32_t)lane < np) st_agent(&view.ready[base + (uint32_t)lane], sh.pend[lane]);
-                if (sk && lane == 0) st_agent(&view.ready[base + np], kDagSkip);
-            }
-        }
         if (wave == 0) {
             uint32_t t = kDagEmpty;
             while (true) {
@@ -434,6 +436,19 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
         const uint32_t t = sh.slot;
         __syncthreads();  // the slot is rewritten only after this barrier
         if (t == kDagEmpty) break;
+        if (N > 0 && wave == helper) {
+            // the previous put's releases: one tail fetch-add for all of them,
+            // while the task runs (a put that released any task kept one, so
+            // wave 0 never waits on the ready list for these: see kept)
+            const uint32_t np = sh.npend, sk = sh.skip;
+            if (np + sk) {
+                uint32_t base = 0;
+                if (lane == 0) base = add_agent(view.tail, np + sk);
+                base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
+                if ((uint32_t)lane < np) st_agent(&view.ready[base + (uint32_t)lane], sh.pend[lane]);
+                if (sk && lane == 0) st_agent(&view.ready[base + np], kDagSkip);
+            }
+        }
         if (!Kind::kSc1Payload) acquire_agent();
         stamp(0);
 #if HX_DAG_TRACE
@@ -514,6 +529,10 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
             }
         }
         if (__syncthreads_or(!ok)) break;
+        // every wave is done with the task: the Kind's between-task work
+        // (e.g. resetting its LDS hand-off flags so the next body needs no
+        // barrier of its own)
+        group_after_body<Kind>(ctx, t);
         stamp(1);
 #if HX_DAG_TRACE
         if (view.trace && threadIdx.x == 0) view.trace[(size_t)t * kDagTraceWords + 2] = __builtin_amdgcn_s_memrealtime();
@@ -572,7 +591,8 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
                 // the kept task's ready slot is appended by the helper wave
                 w.skip_lane = 0;
             }
-            __syncthreads();  // sh.pend / npend / skip before the helper reads them
+            // (sh.pend / npend / skip reach the helper through the next
+            // task's slot barrier)
         } else {
             if (wave == 0) {
                 Kind::put(ctx, w, t);

@@ -54,10 +54,8 @@ while t != 0:
                  # 0 / 1 done, egress done (sw.hip SwDagWgKind stamps)
                  "in_ingress": ns(tr[t, 8] - tr[t, 1]), "in_wave0": ns(tr[t, 10] - tr[t, 1]),
                  "in_wave1": ns(tr[t, 11] - tr[t, 1]), "in_egress": ns(tr[t, 9] - tr[t, 1]),
-                 # wave 0's loop start, after its first chunk (steps 0-63) and
-                 # its third (steps 128-191); wave 1's loop start
-                 "in_w0_loop": ns(tr[t, 12] - tr[t, 1]), "in_w0_c1": ns(tr[t, 13] - tr[t, 1]),
-                 "in_w0_c3": ns(tr[t, 14] - tr[t, 1]), "in_w1_loop": ns(tr[t, 15] - tr[t, 1])})
+                 # waves 0 / 1: loop start (prologue done)
+                 "in_w0_loop": ns(tr[t, 12] - tr[t, 1]), "in_w1_loop": ns(tr[t, 15] - tr[t, 1])})
     t = r
 hops.reverse()
 total = ns(tr[ntw * nth - 1, 2] - t0)
@@ -68,8 +66,8 @@ for kind in ("row", "col", "diag", "all"):
     if not hs:
         continue
     res[kind] = {"hops": len(hs), "kept": sum(h["kept"] for h in hs)}
-    for k in ("release", "pickup", "body", "put", "in_ingress", "in_w0_loop", "in_w0_c1", "in_w0_c3", "in_wave0",
-              "in_w1_loop", "in_wave1", "in_egress"):
+    for k in ("release", "pickup", "body", "put", "in_ingress", "in_w0_loop", "in_wave0", "in_w1_loop", "in_wave1",
+              "in_egress"):
         v = np.array([h[k] for h in hs])
         res[kind][k + "_us"] = round(float(v.mean()) / 1e3, 3)
         res[kind][k + "_ms_total"] = round(float(v.sum()) / 1e6, 3)
