@@ -567,10 +567,14 @@ __global__ __launch_bounds__(64) void k_sw_rows(SwCtx c) {
 constexpr int kSwRing = 512;  // columns per inter-wave ring (+1 wrap slot)
 constexpr int kSwRingStride = kSwRing + 4;
 constexpr int kSwSub = 16;    // steps per hand-off
+// dummy ring slots per compute wave (its lanes 0..62 write there every step
+// while lane 63 writes the out ring; lane stride 1: neighbours' two-dword
+// writes overlap. HX_SW_EXP 4: stride 2, no overlap)
+constexpr int kSwDummy = HX_SW_EXP == 4 ? 256 : 128;
 
 __host__ __device__ inline size_t sw_band_lds_bytes(int nw) {
     return (size_t)(nw + 1) * kSwRingStride * 4  // rings
-           + (size_t)nw * 128 * 4                 // per-wave dummy slots (lanes 0..62's ring writes)
+           + (size_t)nw * kSwDummy * 4            // per-wave dummy slots (lanes 0..62's ring writes)
            + (size_t)nw * 2048                    // per-wave code rings: 4 byte-shifted copies, double-mapped
            + 2 * 64 * 4;                          // prod / cons words
 }
@@ -917,7 +921,7 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
         mr[q] = sw_row2(c.s2[r - 1 + q]);
         lr[q] = left_h(r + q) + (r + q) + C0;
     }
-    int *wbase = lane == 63 ? ring_out : dummy + w * 128 + lane;
+    int *wbase = lane == 63 ? ring_out : dummy + w * kSwDummy + (HX_SW_EXP == 4 ? 2 * lane : lane);
     const int8_t *s1 = c.s1 + C0;
     // s1 code (1..4) of column x; loads clamped to the band, never predicated,
     // so that nothing waits for them before their use
@@ -1043,7 +1047,7 @@ __global__ __launch_bounds__(1024) void k_sw_band_rows(SwCtx c) {
     const int bpt = c.th / c.bh, k = nwave / bpt;
     int *rings = sw_lds;
     int *dummy = rings + (size_t)(nwave + 1) * kSwRingStride;
-    uint8_t *code_rings = (uint8_t *)(dummy + nwave * 128);
+    uint8_t *code_rings = (uint8_t *)(dummy + nwave * kSwDummy);
     int *prod = (int *)(code_rings + nwave * 2048), *cons = prod + 64;
     const size_t gstride = (size_t)c.ntw * c.tw;  // granules per tile row
     bool ok = true;
@@ -1135,7 +1139,7 @@ struct SwDagWgKind {
         const int nw = c.th / c.bh;
         int *rings = sw_lds;
         int *dummy = rings + (size_t)(nw + 1) * kSwRingStride;
-        uint8_t *code_rings = (uint8_t *)(dummy + nw * 128);
+        uint8_t *code_rings = (uint8_t *)(dummy + nw * kSwDummy);
         int *prod = (int *)(code_rings + nw * 2048), *cons = prod + 64;
         // the workgroup's last tile: its right column (two buffers by tile
         // parity) and its right neighbour's corner, for a row successor
@@ -1200,7 +1204,7 @@ struct SwDagWgKind {
     __device__ static int *flags_of(const SwCtx &c) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
         const int nw = c.th / c.bh;
-        return (int *)((uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * 128) + nw * 2048);
+        return (int *)((uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * kSwDummy) + nw * 2048);
     }
     // right column, bottom row, corner (:212-226): run_dag_group's split put
     // (waiters prefetched while the tile runs, one release for all three)
@@ -1213,7 +1217,7 @@ struct SwDagWgKind {
     __device__ static void datums(const SwCtx &c, uint32_t t, unsigned long long (&d)[3]) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
         const int nw = c.th / c.bh;
-        const int *last = (const int *)((const uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * 128) +
+        const int *last = (const int *)((const uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * kSwDummy) +
                                         nw * 2048) + 128;
         (void)t;
         d[0] = 0ull;
@@ -1226,7 +1230,7 @@ __global__ __launch_bounds__(1024) void k_sw_dag_wg(SwCtx c, DagView v) {
     extern __shared__ __attribute__((aligned(16))) int sw_lds[];
     __shared__ uint32_t task_slot;
     const int nw = c.th / c.bh;
-    int *prod = (int *)((uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * 128) + nw * 2048);
+    int *prod = (int *)((uint8_t *)(sw_lds + (size_t)(nw + 1) * kSwRingStride + nw * kSwDummy) + nw * 2048);
     int *last = prod + 128;
     if (threadIdx.x < 128) prod[threadIdx.x] = 0;  // prod / cons (after_body resets them between tiles)
     if (threadIdx.x == 0) *last = -2;  // no tile yet (run_dag_group's first barrier orders these)

@@ -55,7 +55,10 @@ struct UtsCtx {
     uint32_t bin_thr;  // BIN trees: a node has m children iff rand < bin_thr (every depth >= 1)
     int nthr;        // words in thr
     int geo_depth;   // kUtsGeoFixed: depths 1..geo_depth-1 use table 0, deeper nodes are leaves
-    uint32_t thr16[16];  // kUtsGeoFixed: thresholds 1..16 of table 0 (kernel arguments: SGPRs)
+    // kUtsGeoFixed: table 0's bucket bytes (kUtsBuckets, see uts_nc): per
+    // 2^21-wide bucket of rand, the thresholds at or below its start (| 0x80
+    // when more than two thresholds fall inside it)
+    const uint32_t *nb;
     const int4 *rules;
     const uint32_t *thr;
     unsigned long long *hist;
@@ -63,6 +66,9 @@ struct UtsCtx {
 
 constexpr size_t kUtsLdsRules = 64;     // depth rules cached in LDS per wave
 constexpr size_t kUtsLdsThr = 4 * 128;  // up to 4 GEO threshold tables
+// kUtsGeoFixed: 1024 buckets of rand (2^21 wide), one byte each, kept in
+// s_thr words 128..383 (a fixed-shape tree has one table: the rest is free)
+constexpr int kUtsBuckets = 1024, kUtsBucketShift = 21;
 
 // LDS copies of the rule tables (file scope, so every access is a ds_read:
 // a generic pointer to them would compile to flat loads whose waits also
@@ -86,15 +92,18 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
     if (MODE == kUtsBin) return r < c.bin_thr ? c.m : 0;
     if (MODE == kUtsGeoFixed) {
         if (d >= c.geo_depth) return 0;
-        int n = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) n += c.thr16[k] <= r ? 1 : 0;
-        if (n == 16) {
-            // thresholds 17..100 of table 0, binary-searched in the LDS copy:
-            // P(n > 16) = 0.8^17 ~ 2.3% per node at b = 4, so ~3 of 4 batches
-            // of 64 have such a lane — a search through device memory (seven
-            // dependent L2 round trips) cost those batches more than their SHA-1
-            int lo = 16, hi = 100;
+        // bucket of rand: the thresholds at or below its start (n_lo), and
+        // the next two compared — exact whenever at most two thresholds fall
+        // inside the bucket (thresholds are sorted): n = #{k : thr[k] <= r}.
+        // 6-8 VALU and two LDS reads per node instead of 16 compares (and a
+        // binary search in 3 of 4 batches at b = 4, where P(n > 16) is 2.3 %)
+        const uint32_t e = ((const uint8_t *)(s_thr + 128))[r >> kUtsBucketShift];
+        const uint32_t nlo = e & 0x7fu;
+        uint32_t n = nlo + (s_thr[nlo + 1] <= r ? 1u : 0u) + (s_thr[nlo + 2] <= r ? 1u : 0u);
+        if (e & 0x80u) {
+            // a dense bucket (thresholds past ~23 at b = 4, P ~ 0.6 % per
+            // node): binary search of the LDS table above n_lo
+            int lo = (int)nlo, hi = 100;
             for (int s = 0; s < 7; ++s) {
                 int mid = (lo + hi + 1) >> 1;
                 if (lo < hi) {
@@ -102,9 +111,9 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
                     else hi = mid - 1;
                 }
             }
-            n = lo;
+            n = (uint32_t)lo;
         }
-        return n;
+        return (int)n;
     }
     constexpr bool LDS = MODE == kUtsRulesLds;
     int ri = d;
@@ -174,6 +183,7 @@ struct UtsKind {
         uint32_t nodes = 0, leaves = 0;
         uint32_t maxd = 0;
         uint32_t trace_seen = 0;  // FEAT 2: the deepest depth this wave has stamped
+        uint32_t mode = 0;        // FEAT 2: 1 while the scheduler runs the narrow loop (hx_sched.h)
         __device__ void flush(SchedGlobals *g) {
             unsigned long long n = wave_sum((unsigned long long)nodes),
                                l = wave_sum((unsigned long long)leaves);
@@ -226,8 +236,10 @@ struct UtsKind {
             const uint32_t dm = wave_max(counted ? (uint32_t)h1 : 0u);
             if (dm > acc.trace_seen) {
                 acc.trace_seen = dm;
+                // the stamp's low bit: reached in the narrow loop (1) or not
                 if (lane_id() == 0 && (int)dm < c.hist_levels)
-                    __hip_atomic_fetch_min(&c.hist[dm], (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                    __hip_atomic_fetch_min(&c.hist[dm],
+                                           ((unsigned long long)__builtin_amdgcn_s_memrealtime() << 1) | acc.mode,
                                            __ATOMIC_RELAXED, HX_AGENT);
             }
         }
@@ -285,8 +297,9 @@ __global__ __launch_bounds__(64 * WPG) void k_uts_search(UtsCtx ctx, PoolView po
         }
     }
     if (MODE == kUtsGeoFixed) {
-        // table 0 in LDS for the rare tail search (uts_nc)
+        // table 0 and its bucket bytes in LDS (uts_nc)
         for (int i = threadIdx.x; i < 128; i += 64 * WPG) s_thr[i] = ctx.thr[i];
+        for (int i = threadIdx.x; i < kUtsBuckets / 4; i += 64 * WPG) s_thr[128 + i] = ctx.nb[i];
     }
     if (MODE == kUtsRulesLds) {
         // the per-node rule lookup becomes LDS-latency (no dependent HBM/L2 loads)
@@ -294,16 +307,6 @@ __global__ __launch_bounds__(64 * WPG) void k_uts_search(UtsCtx ctx, PoolView po
         for (int i = threadIdx.x; i < ctx.nthr; i += 64 * WPG) s_thr[i] = ctx.thr[i];
     }
     __syncthreads();
-    if (MODE == kUtsGeoFixed) {
-        // the 16 thresholds compared per node live in VGPRs (wave-uniform
-        // values the compiler would otherwise keep in SGPRs, spilling the
-        // scheduler's scalar state around the batch loop)
-        UtsCtx lc = ctx;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) asm volatile("v_mov_b32 %0, %1" : "=v"(lc.thr16[k]) : "s"(ctx.thr16[k]));
-        run_worker<K, kUtsCap, GLOBAL, WPG>(lc, pool, g, cfg, st[wave], worker == 0, ib, wave, worker);
-        return;
-    }
     run_worker<K, kUtsCap, GLOBAL, WPG>(ctx, pool, g, cfg, st[wave], worker == 0, ib, wave, worker);
 }
 
@@ -557,10 +560,28 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         tab.dmem = nullptr;
         HX_TRY(build_tables(*params, tab.T));
         const size_t rb = tab.T.rules.size() * sizeof(int4), tb = tab.T.thr.size() * 4;
-        HX_HIP(hipMalloc(&tab.dmem, ((rb + 255) & ~(size_t)255) + tb + 256));
+        HX_HIP(hipMalloc(&tab.dmem, ((rb + 255) & ~(size_t)255) + ((tb + 255) & ~(size_t)255) + kUtsBuckets + 256));
         char *dp = (char *)tab.dmem;
         HX_HIP(hipMemcpy(dp, tab.T.rules.data(), rb, hipMemcpyHostToDevice));
         HX_HIP(hipMemcpy(dp + ((rb + 255) & ~(size_t)255), tab.T.thr.data(), tb, hipMemcpyHostToDevice));
+        // table 0's bucket bytes (kUtsGeoFixed, uts_nc): per bucket
+        // [b 2^21, (b+1) 2^21) of rand, n_lo = #{k : thr[k] <= b 2^21} and
+        // 0x80 when more than two thresholds lie strictly inside it
+        uint8_t nb[kUtsBuckets] = {0};
+        if (tab.T.thr.size() >= 128) {
+            const uint32_t *t0 = tab.T.thr.data();
+            for (int b = 0; b < kUtsBuckets; ++b) {
+                const uint64_t lo = (uint64_t)b << kUtsBucketShift, hi = (uint64_t)(b + 1) << kUtsBucketShift;
+                int nlo = 0, inside = 0;
+                for (int k = 1; k <= 100; ++k) {
+                    nlo += t0[k] <= lo;
+                    inside += t0[k] > lo && t0[k] < hi;
+                }
+                nb[b] = (uint8_t)(nlo | (inside > 2 ? 0x80 : 0));
+            }
+        }
+        HX_HIP(hipMemcpy(dp + ((rb + 255) & ~(size_t)255) + ((tb + 255) & ~(size_t)255), nb, kUtsBuckets,
+                         hipMemcpyHostToDevice));
         tab.p = *params;
         tab.device = m.device;
         tab.have = true;
@@ -568,6 +589,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     const UtsTables &T = tab.T;
     int4 *d_rules = (int4 *)tab.dmem;
     uint32_t *d_thr = (uint32_t *)((char *)tab.dmem + ((T.rules.size() * sizeof(int4) + 255) & ~(size_t)255));
+    const uint32_t *d_nb = (const uint32_t *)((char *)d_thr + ((T.thr.size() * 4 + 255) & ~(size_t)255));
 
     // the optional per-level histogram
     const size_t hb = (size_t)max_levels * 8;
@@ -606,7 +628,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         if (rest_zero && T.thr.size() >= 128) geo_depth = d;
     }
     ctx.geo_depth = geo_depth;
-    for (int k = 0; k < 16; ++k) ctx.thr16[k] = geo_depth ? T.thr[1 + k] : 0u;
+    ctx.nb = d_nb;
 
     PoolView pool;
     const uint32_t nq = (uint32_t)env_int("HCLIB_HIP_DEQUES", 64);

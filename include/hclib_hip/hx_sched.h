@@ -44,6 +44,8 @@
 // (hx_common.h). Every spin is bounded.
 #pragma once
 
+#include <type_traits>
+
 #include "hx_common.h"
 
 namespace hx {
@@ -805,6 +807,17 @@ struct NarrowState {
 #else
 #define HX_NARROW_ATTR __forceinline__
 #endif
+// Optional diagnostic: a Kind's Acc with a `mode` field learns whether its
+// tasks run in the narrow loop (1) or the main loop (0).
+template <class A, class = void>
+struct acc_has_mode : std::false_type {};
+template <class A>
+struct acc_has_mode<A, decltype((void)A::mode)> : std::true_type {};
+template <class A>
+__device__ __forceinline__ void acc_set_mode(A &a, uint32_t m) {
+    if constexpr (acc_has_mode<A>::value) a.mode = m;
+}
+
 template <class Kind, int CAP>
 __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
     const typename Kind::Ctx &ctx_ref, typename Kind::Acc &acc_ref, uint32_t *err, WaveStack<Kind, CAP> &st,
@@ -815,6 +828,7 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
     // the parameters and store the counters (flat memory, waited on mid-task)
     const typename Kind::Ctx ctx = ctx_ref;
     typename Kind::Acc acc = acc_ref;
+    acc_set_mode(acc, 1u);
     const uint32_t lane = (uint32_t)lane_id();
     uint32_t carry = lane0(ns.carry), batches = 0;
     while (true) {
@@ -867,6 +881,7 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
     }
     ns.carry = carry;
     ns.batches = batches;
+    acc_set_mode(acc, 0u);
     acc_ref = acc;
     return ns;
 }

@@ -1,0 +1,49 @@
+"""Same-box A/B of library builds (development aid): each named build runs
+the same workloads in its own process, alternating, best of 3 each:
+python scripts/ab_libs.py name=path/to/libhclib_amd.so ... [-- workload ...]
+Workloads: T1 T1L T1XL T3L sw_rows sw_dag fib30."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TREES = {"T1": ("-t 1 -a 3 -d 10 -b 4 -r 19", 4130071), "T1L": ("-t 1 -a 3 -d 13 -b 4 -r 29", 102181082),
+         "T1XL": ("-t 1 -a 3 -d 15 -b 4 -r 29", 1635119272), "T3L": ("-t 0 -b 2000 -q 0.200014 -m 5 -r 7", 111345631)}
+CHILD = r'''
+import os, sys, json
+sys.path.insert(0, sys.argv[1])
+import hclib_amd as H
+H.init(0)
+TREES = json.loads(sys.argv[2]); out = {}
+for w in sys.argv[3:]:
+    best = None
+    for _ in range(3):
+        if w in TREES:
+            r = H.uts(TREES[w][0]); assert r["nodes"] == TREES[w][1], (w, r["nodes"]); ms = r["kernel_ms"]
+        elif w.startswith("sw_"):
+            s1 = H.sw_map(open(os.path.join(sys.argv[1], "tests/golden/sw/string1-huge.txt"), "rb").read())[:65536]
+            s2 = H.sw_map(open(os.path.join(sys.argv[1], "tests/golden/sw/string2-huge.txt"), "rb").read())[:65536]
+            os.environ["HCLIB_HIP_SW_SCHED"] = w[3:]
+            sc, st = H.sw(s1, s2, 256, 256); assert sc == 128772; ms = st["kernel_ms"]
+        else:
+            v, st = H.fib(30); assert v == 832040; ms = st["kernel_ms"]
+        best = ms if best is None else min(best, ms)
+    out[w] = round(best, 3)
+print(json.dumps(out))
+'''
+args = sys.argv[1:]
+work = ["T1", "T1L", "T1XL", "T3L", "sw_rows", "sw_dag", "fib30"]
+if "--" in args:
+    i = args.index("--")
+    args, work = args[:i], args[i + 1:]
+libs = [a.split("=", 1) for a in args]
+for rep in range(2):
+    for name, path in libs:
+        env = dict(os.environ, HCLIB_AMD_LIB=os.path.abspath(path))
+        r = subprocess.run([sys.executable, "-c", CHILD, ROOT, json.dumps(TREES)] + work, env=env,
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode:
+            print(name, "FAILED", r.stderr[-2000:], flush=True)
+            sys.exit(1)
+        print(f"rep {rep} {name:10s} {r.stdout.strip()}", flush=True)

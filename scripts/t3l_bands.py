@@ -27,13 +27,17 @@ width = np.array(plain[0]["levels"], dtype=np.int64)
 os.environ["HCLIB_HIP_UTS_TRACE"] = "1"
 r = H.uts(a.tree, max_levels=levels)
 del os.environ["HCLIB_HIP_UTS_TRACE"]
-t = np.array(r["levels"], dtype=np.float64)
+raw = np.array(r["levels"], dtype=np.uint64)
 # depth 0 is not stamped (the root comes from roots(), which counts into
-# slot 0 instead): the leading edge starts at depth 1
-t[0] = t[1]
-ok = t < 2 ** 63
+# slot 0 instead): the leading edge starts at depth 1. A stamp is
+# (100 MHz time << 1) | 1 when the batch that reached the depth ran in the
+# scheduler's narrow-frontier loop
+raw[0] = raw[1]
+ok = raw < np.uint64(2 ** 63)
 depth = int(ok.sum())
-t = (t[:depth] - t[:depth].min()) * 10.0  # ns
+narrow = (raw[:depth] & np.uint64(1)).astype(bool)
+t = (raw[:depth] >> np.uint64(1)).astype(np.float64)
+t = (t - t.min()) * 10.0  # ns
 step = np.diff(t)  # step[d] = time from reaching depth d to depth d + 1
 ghz = 2.4
 print(json.dumps({"tree": a.tree, "plain_ms": [round(p["kernel_ms"], 3) for p in plain],
@@ -59,5 +63,11 @@ for lo, hi in [(0, 64), (64, 256), (256, 1024), (1024, 4096), (4096, 10 ** 9)]:
     if m.any():
         print(json.dumps({"width": [lo, hi], "levels": int(m.sum()), "ns_per_level": round(float(step[m].mean()), 1),
                           "ms": round(float(step[m].sum()) / 1e6, 3)}), flush=True)
+# step into depth d + 1 by how depth d + 1 was first reached
+nx = narrow[1:depth]
+print(json.dumps({"reached_in_narrow_loop": {"levels": int(nx.sum()), "ns_per_level": round(float(step[nx].mean()), 1),
+                                             "ms": round(float(step[nx].sum()) / 1e6, 3)},
+                  "reached_in_main_loop": {"levels": int((~nx).sum()), "ns_per_level": round(float(step[~nx].mean()), 1),
+                                           "ms": round(float(step[~nx].sum()) / 1e6, 3)}}), flush=True)
 print(json.dumps({"summary": True, "excess_ms_total": round(tot_excess / ghz / 1e6, 3),
                   "worst_band": worst["depths"]}), flush=True)
