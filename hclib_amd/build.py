@@ -37,7 +37,8 @@ CFLAGS = [
 
 VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "trace": ["-DHX_TRACE=1"],
             # SW band-sweep timing experiments (wrong results by design: sw.hip HX_SW_EXP)
-            "swexp1": ["-DHX_SW_EXP=1"], "swexp2": ["-DHX_SW_EXP=2"], "swexp3": ["-DHX_SW_EXP=3"], "swexp4": ["-DHX_SW_EXP=4"], "strict": ["-DHX_STRICT_HANDOFF=1"],
+            "swexp1": ["-DHX_SW_EXP=1"], "swexp2": ["-DHX_SW_EXP=2"], "swexp3": ["-DHX_SW_EXP=3"], "swexp4": ["-DHX_SW_EXP=4"],
+            "shift": ["-DHX_SW_SHIFT=1"], "strict": ["-DHX_STRICT_HANDOFF=1"],
             "narrow_noinline": ["-DHX_NARROW_NOINLINE=1"],
             "sched_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
             "sched_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],

@@ -94,6 +94,14 @@ __device__ __forceinline__ int shift_up1(int v) {
 #ifndef HX_SW_EXP
 #define HX_SW_EXP 0
 #endif
+// 64-step band hand-offs gather lane 63's outputs by DPP (1) or store them
+// to the ring every step from every lane (0, default). Measured same-box
+// (profiles/r03/sw_shift_ab.log): the one-tile-row sweep 57 -> 55 cycles per
+// step at R = 2 (48 -> 45 at R = 1), but the DAG 8.12 -> 8.55 ms (its
+// consumer wave receives each chunk in one burst at the chunk's end)
+#ifndef HX_SW_SHIFT
+#define HX_SW_SHIFT 0
+#endif
 __device__ __forceinline__ unsigned long long sw_stamp() {
 #if HX_STAMPS
     unsigned long long t;
@@ -636,9 +644,15 @@ __device__ __forceinline__ void lds_flag_st(int *p, int v) {
 // cells (see sw_tile). left = h one step back, o2 = h two steps back (S = 2).
 // Operands of 4 steps are read two groups ahead, in program order before the
 // previous group's ring writes.
-template <bool MASK, int S, int K>
+// SHIFT (64-step hand-offs): lane 63's outputs are not written to the ring
+// step by step (one LDS store per step, issued by every lane — measured 14-16
+// cycles of a lone wave's step, scripts/ubench/ub_swstep.hip) but shifted into
+// `acc` by one DPP per step (wave_shl:1, lane 63 taking the new value), so
+// after the 64 steps lane j holds step j's output and one store per chunk
+// writes them all (sw_band_row).
+template <bool MASK, int S, int K, bool SHIFT = false>
 __device__ __forceinline__ void sw_band_sub(int s, int ncols, const int *top4, const uint32_t *code4, int *wb,
-                                            uint32_t mrow, int &left, int &diag, int &o2) {
+                                            uint32_t mrow, int &left, int &diag, int &o2, int &acc) {
     constexpr int G = K / 4;
     const int lane = lane_id();
     int4 tn = *(const int4 *)top4, tn2 = *(const int4 *)(top4 + 4);
@@ -672,7 +686,8 @@ __device__ __forceinline__ void sw_band_sub(int s, int ncols, const int *top4, c
             }
             if (S == 2) o2 = left;
             left = h;
-            wb[k] = h;
+            if (SHIFT) acc = __builtin_amdgcn_update_dpp(h, acc, 0x130, 0xf, 0xf, false);
+            else wb[k] = h;
         }
     }
 }
@@ -682,9 +697,9 @@ __device__ __forceinline__ void sw_band_sub(int s, int ncols, const int *top4, c
 // comes from lane L-1's last row, each other row's from the row before it in
 // the same column. One DPP shift and one ring write serve R cells, and a
 // 256-row tile needs 4 / R waves, so fewer hand-off lags are paid.
-template <bool MASK, int K, int R>
+template <bool MASK, int K, int R, bool SHIFT = false>
 __device__ __forceinline__ void sw_band_subR(int s, int ncols, const int *top4, const uint32_t *code4, int *wb,
-                                             const uint32_t (&mrow)[R], int (&lr)[R], int &diag) {
+                                             const uint32_t (&mrow)[R], int (&lr)[R], int &diag, int &acc) {
     constexpr int G = K / 4;
     const int lane = lane_id();
     int4 tn = HX_SW_EXP == 2 ? make_int4(s, s, s, s) : *(const int4 *)top4,
@@ -721,7 +736,8 @@ __device__ __forceinline__ void sw_band_subR(int s, int ncols, const int *top4, 
                 up = h;
             }
             diag = MASK ? (v ? up0 : diag) : up0;
-            if (HX_SW_EXP != 1 || lane == 63) wb[k] = lr[R - 1];
+            if (SHIFT) acc = __builtin_amdgcn_update_dpp(lr[R - 1], acc, 0x130, 0xf, 0xf, false);
+            else if (HX_SW_EXP != 1 || lane == 63) wb[k] = lr[R - 1];
         }
     }
 }
@@ -940,6 +956,10 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
     const int cofs = (S * lane) & 3;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = true;
+    // 64-step hand-offs with one row of skew: lane 63's outputs gathered by
+    // DPP (sw_band_sub SHIFT) and stored once per chunk
+    constexpr bool kShift = K == 64 && S == 1 && HX_SW_SHIFT;
+    int acc = 0;
     // (trace builds: the loop start only — a stamp inside the loop, an SMEM
     // read, waits for every LDS operation in flight and slows the sweep)
     if (HX_DAG_TRACE && B.trec && lane == 0 && w < 2) B.trec[w == 0 ? 12 : 15] = __builtin_amdgcn_s_memrealtime();
@@ -973,17 +993,22 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
             phase(1);
             if (R > 1) {
                 if (full)
-                    sw_band_subR<false, K, R>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mr, lr,
-                                              diag);
+                    sw_band_subR<false, K, R, kShift>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K,
+                                                      mr, lr, diag, acc);
                 else
-                    sw_band_subR<true, K, R>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mr, lr,
-                                             diag);
+                    sw_band_subR<true, K, R, kShift>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K,
+                                                     mr, lr, diag, acc);
             } else if (full) {
-                sw_band_sub<false, S, K>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mrow, left,
-                                         diag, o2);
+                sw_band_sub<false, S, K, kShift>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mrow,
+                                                 left, diag, o2, acc);
             } else {
-                sw_band_sub<true, S, K>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mrow, left,
-                                        diag, o2);
+                sw_band_sub<true, S, K, kShift>(s, ncols, ring_in + slot + q * K, cb + q * (K / 4), wb + q * K, mrow,
+                                                left, diag, o2, acc);
+            }
+            if (kShift) {
+                // the chunk's 64 outputs of lane 63 (columns s0 - D .. s0 + 63
+                // - D), one per lane: the slots the per-step stores filled
+                ring_out[((s0 - D) & (kSwRing - 1)) + lane] = acc;
             }
             phase(0);
             // lane 63's last S columns of the chunk may have gone past the
@@ -1282,8 +1307,10 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     // three), the row schedule to four (one band per 256-row tile row: the
     // per-row wavefront lag is paid once per 256 rows). SW-64K measured
     // (profiles/r02/sw_forms.log): rows 12: 4.4 ms, 212: 3.55, 412: 3.50;
-    // dag 12: 11.2, 212: 9.4, 412: 9.6
-    const int form = sw_pick_form(th, dag ? 212 : 412), bh = sw_form_bh(form);
+    // dag 12: 11.2, 212: 9.4, 412: 9.6. Round 3, same box
+    // (profiles/r03/sw_forms_k64.log): hand-offs every 64 steps for the DAG's
+    // tiles, 212: 8.35 -> 214: 8.12-8.14 ms; rows 414 3.56 vs 412 3.49-3.51
+    const int form = sw_pick_form(th, dag ? 214 : 412), bh = sw_form_bh(form);
     const bool band_shape = sw_band_ok(th, bh) && tw <= 65536;
     const bool band = rows && band_shape && !(sched && !strcmp(sched, "rows1"));
     const size_t nt = ntw * nth;

@@ -46,8 +46,48 @@
                  "v_max3_i32 %2, %2, %1, %3"                                 \
                  : "+v"(u), "+v"(h0), "+v"(h1), "+v"(d), "+v"(o))
 
+// R = 1 step with the band loop's side work: + an independent
+// v_add_u32_sdwa (the diagonal + score), + a ds_write_b32 of h (the ring
+// write every lane issues), + both
+#define STEP_DPP1A                                                          \
+    asm volatile("s_nop 1\n v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf\n" \
+                 "v_add_u32_sdwa %2, %0, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n" \
+                 "v_max3_i32 %1, %1, %0, %2"                                 \
+                 : "+v"(u), "+v"(h0), "+v"(d)                                \
+                 : "v"(o))
+#define STEP_DPP1W                                                          \
+    asm volatile("s_nop 1\n v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf\n" \
+                 "v_max3_i32 %1, %1, %0, %2\n"                               \
+                 "ds_write_b32 %3, %1"                                        \
+                 : "+v"(u), "+v"(h0)                                         \
+                 : "v"(d), "v"(la)                                           \
+                 : "memory")
+#define STEP_DPP1AW                                                         \
+    asm volatile("s_nop 1\n v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf\n" \
+                 "v_add_u32_sdwa %2, %0, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n" \
+                 "v_max3_i32 %1, %1, %0, %2\n"                               \
+                 "ds_write_b32 %4, %1"                                        \
+                 : "+v"(u), "+v"(h0), "+v"(d)                                \
+                 : "v"(o), "v"(la)                                           \
+                 : "memory")
+
+// the ring write one step late: h of the previous step, written right after
+// the DPP that already waited for it (two registers alternate)
+#define STEP_DPP1WL                                                         \
+    asm volatile("s_nop 1\n v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf\n" \
+                 "ds_write_b32 %4, %1\n"                                     \
+                 "v_max3_i32 %2, %1, %0, %3\n"                               \
+                 "s_nop 1\n v_mov_b32_dpp %0, %2 wave_shr:1 row_mask:0xf bank_mask:0xf\n" \
+                 "ds_write_b32 %4, %2 offset:256\n"                          \
+                 "v_max3_i32 %1, %2, %0, %3"                                 \
+                 : "+v"(u), "+v"(h0), "+v"(h1)                               \
+                 : "v"(d), "v"(la)                                           \
+                 : "memory")
+
 template <int MODE>
 __global__ void k_step(int *io, unsigned long long *cyc, int n) {
+    __shared__ int lds[512];
+    const uint32_t la = (uint32_t)(uintptr_t)&lds[threadIdx.x];
     const int g = threadIdx.x;
     int u = io[g], h0 = io[g + 64], h1 = io[g + 128], h2 = io[g + 192], h3 = io[g + 256], d = io[g + 320],
         o = io[g + 384];
@@ -61,10 +101,15 @@ __global__ void k_step(int *io, unsigned long long *cyc, int n) {
             if (MODE == 3) STEP_DPP4;
             if (MODE == 4) STEP_ROW2;
             if (MODE == 5) STEP_FAR2;
+            if (MODE == 6) STEP_DPP1A;
+            if (MODE == 7) STEP_DPP1W;
+            if (MODE == 8) STEP_DPP1AW;
+            if (MODE == 9 && (r & 1) == 0) STEP_DPP1WL;  // two steps per macro
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    io[512 + g] = u ^ h0 ^ h1 ^ h2 ^ h3 ^ o;
+    __syncthreads();
+    io[512 + g] = u ^ h0 ^ h1 ^ h2 ^ h3 ^ o ^ lds[(g + 1) & 63];
     if (g == 0) cyc[0] = t1 - t0;
 }
 
@@ -97,5 +142,9 @@ int main() {
     run<3>("dpp4");
     run<4>("row_shr");
     run<5>("dppfar");
+    run<6>("dpp1+add");
+    run<7>("dpp1+ds");
+    run<8>("dpp1+add+ds");
+    run<9>("dpp1+ds late");
     return 0;
 }
