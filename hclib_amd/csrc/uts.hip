@@ -184,6 +184,7 @@ struct UtsKind {
         uint32_t maxd = 0;
         uint32_t trace_seen = 0;  // FEAT 2: the deepest depth this wave has stamped
         uint32_t mode = 0;        // FEAT 2: 1 while the scheduler runs the narrow loop (hx_sched.h)
+        uint32_t wid = 0;         // FEAT 2: this worker's id (hx_sched.h acc_set_wid)
         __device__ void flush(SchedGlobals *g) {
             unsigned long long n = wave_sum((unsigned long long)nodes),
                                l = wave_sum((unsigned long long)leaves);
@@ -236,10 +237,12 @@ struct UtsKind {
             const uint32_t dm = wave_max(counted ? (uint32_t)h1 : 0u);
             if (dm > acc.trace_seen) {
                 acc.trace_seen = dm;
-                // the stamp's low bit: reached in the narrow loop (1) or not
+                // stamp = time << 17 | worker (16 bits) << 1 | reached in the
+                // narrow loop (1) or not
                 if (lane_id() == 0 && (int)dm < c.hist_levels)
                     __hip_atomic_fetch_min(&c.hist[dm],
-                                           ((unsigned long long)__builtin_amdgcn_s_memrealtime() << 1) | acc.mode,
+                                           ((unsigned long long)__builtin_amdgcn_s_memrealtime() << 17) |
+                                               ((unsigned long long)(acc.wid & 0xffffu) << 1) | acc.mode,
                                            __ATOMIC_RELAXED, HX_AGENT);
             }
         }

@@ -817,6 +817,15 @@ template <class A>
 __device__ __forceinline__ void acc_set_mode(A &a, uint32_t m) {
     if constexpr (acc_has_mode<A>::value) a.mode = m;
 }
+// ... and a `wid` field the running worker's id (diagnostic traces)
+template <class A, class = void>
+struct acc_has_wid : std::false_type {};
+template <class A>
+struct acc_has_wid<A, decltype((void)A::wid)> : std::true_type {};
+template <class A>
+__device__ __forceinline__ void acc_set_wid(A &a, uint32_t w) {
+    if constexpr (acc_has_wid<A>::value) a.wid = w;
+}
 
 template <class Kind, int CAP>
 __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
@@ -1007,6 +1016,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     uint32_t rng = 0x9e3779b9u ^ (gid * 0x85ebca6bu + 1u);
 
     typename Kind::Acc acc;
+    acc_set_wid(acc, gid);
     uint32_t bot = 0, top = 0;
     bool active = false;
     uint32_t spins = 0;

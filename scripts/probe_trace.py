@@ -15,8 +15,8 @@ T3L = "-t 0 -b 2000 -q 0.200014 -m 5 -r 7"
 plain = min(H.uts(T3L)["kernel_ms"] for _ in range(3))
 os.environ["HCLIB_HIP_UTS_TRACE"] = "1"
 r = H.uts(T3L, max_levels=17845)
-t = (np.array(r["levels"], dtype=np.uint64) >> np.uint64(1)).astype(np.float64)  # low bit: narrow loop
-ok = t < 2 ** 62
+t = (np.array(r["levels"], dtype=np.uint64) >> np.uint64(17)).astype(np.float64)  # low bits: worker, narrow
+ok = t < 2 ** 46
 t = (t[ok] - t[ok].min()) * 10.0  # ns (100 MHz)
 d = np.diff(t)
 print(f"plain {plain:.2f} ms, traced {r['kernel_ms']:.2f} ms, depths stamped {ok.sum()}, "

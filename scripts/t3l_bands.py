@@ -30,13 +30,14 @@ del os.environ["HCLIB_HIP_UTS_TRACE"]
 raw = np.array(r["levels"], dtype=np.uint64)
 # depth 0 is not stamped (the root comes from roots(), which counts into
 # slot 0 instead): the leading edge starts at depth 1. A stamp is
-# (100 MHz time << 1) | 1 when the batch that reached the depth ran in the
-# scheduler's narrow-frontier loop
+# (100 MHz time << 17) | worker << 1 | 1 when the batch that reached the
+# depth ran in the scheduler's narrow-frontier loop
 raw[0] = raw[1]
 ok = raw < np.uint64(2 ** 63)
 depth = int(ok.sum())
 narrow = (raw[:depth] & np.uint64(1)).astype(bool)
-t = (raw[:depth] >> np.uint64(1)).astype(np.float64)
+wid = ((raw[:depth] >> np.uint64(1)) & np.uint64(0xffff)).astype(np.int64)
+t = (raw[:depth] >> np.uint64(17)).astype(np.float64)
 t = (t - t.min()) * 10.0  # ns
 step = np.diff(t)  # step[d] = time from reaching depth d to depth d + 1
 ghz = 2.4
@@ -69,5 +70,13 @@ print(json.dumps({"reached_in_narrow_loop": {"levels": int(nx.sum()), "ns_per_le
                                              "ms": round(float(step[nx].sum()) / 1e6, 3)},
                   "reached_in_main_loop": {"levels": int((~nx).sum()), "ns_per_level": round(float(step[~nx].mean()), 1),
                                            "ms": round(float(step[~nx].sum()) / 1e6, 3)}}), flush=True)
+# the leading edge moving to another worker between consecutive depths
+same = wid[1:depth] == wid[:depth - 1]
+print(json.dumps({"edge_stays_on_worker": {"levels": int(same.sum()), "ns_per_level": round(float(step[same].mean()), 1),
+                                           "ms": round(float(step[same].sum()) / 1e6, 3)},
+                  "edge_moves_to_another_worker": {"levels": int((~same).sum()),
+                                                   "ns_per_level": round(float(step[~same].mean()), 1),
+                                                   "ms": round(float(step[~same].sum()) / 1e6, 3)},
+                  "distinct_workers_on_edge": int(len(set(wid[1:depth].tolist())))}), flush=True)
 print(json.dumps({"summary": True, "excess_ms_total": round(tot_excess / ghz / 1e6, 3),
                   "worst_band": worst["depths"]}), flush=True)
