@@ -448,6 +448,11 @@ def main():
 
     be = args.backend
     rank, world, local = dist.init_from_env(be, share_device=args.share_device)
+    if args.share_device and world > 1:
+        # a rehearsal with every rank on one GPU: the ranks' persistent grids
+        # must be resident together, else a work-sharing launch
+        # waits for a rank whose kernel cannot start
+        os.environ.setdefault("HCLIB_HIP_WAVES_PER_CU", "2")
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     import hclib_amd as H
