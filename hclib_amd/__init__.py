@@ -79,6 +79,7 @@ EXPORTS_HIP = [
     "hclib_hip_init", "hclib_hip_finalize", "hclib_hip_last_error", "hclib_hip_num_cus",
     "hclib_hip_version", "hclib_hip_forasync", "hclib_hip_forasync_triad_f32",
     "hclib_hip_num_workers", "hclib_hip_uts_search", "hclib_hip_uts_num_children_host",
+    "hclib_hip_uts_bucket_check", "hclib_hip_sha1_calibrate",
     "hclib_hip_fib", "hclib_hip_sw", "hclib_hip_last_sched_counters", "hclib_hip_last_narrow_counters",
     "hclib_hip_sw_band_begin", "hclib_hip_sw_band_rows", "hclib_hip_sw_band_end",
 ]
@@ -121,6 +122,7 @@ def lib():
                                                  C.POINTER(C.c_double)]
         L.hclib_hip_sha1_calibrate.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double),
                                                C.POINTER(C.c_double)]
+        L.hclib_hip_uts_bucket_check.argtypes = [C.POINTER(UtsParams), C.c_uint64, C.POINTER(C.c_uint64)]
         L.hclib_hip_global_bytes.restype = C.c_size_t
         L.hclib_hip_global_bytes.argtypes = [C.c_uint32]
         L.hclib_hip_global_init.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
@@ -209,6 +211,19 @@ def uts(params, shard: int = 0, nshards: int = 1, split_depth: int = 0, max_leve
     if hist is not None:
         out["levels"] = list(hist)
     return out
+
+
+def uts_bucket_check(params, nrandom: int = 1 << 20):
+    """Host check (no GPU) of the bucketed numChildren lookup the fixed-shape
+    GEO kernels use: (mismatches, values compared)."""
+    if isinstance(params, str):
+        params = parse_uts_args(params)
+    n = C.c_uint64()
+    bad = lib().hclib_hip_uts_bucket_check(C.byref(params), nrandom, C.byref(n))
+    if bad < 0:
+        raise HclibError(f"hclib_hip_uts_bucket_check failed ({bad}): "
+                         f"{lib().hclib_hip_last_error().decode(errors='replace')}")
+    return bad, n.value
 
 
 def uts_num_children_host(params, height: int, state_words) -> int:

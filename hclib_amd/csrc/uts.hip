@@ -505,6 +505,40 @@ static int build_tables(const hclib_hip_uts_params_t &p, UtsTables &T) {
     return HCLIB_HIP_OK;
 }
 
+// table 0's bucket bytes (kUtsGeoFixed, uts_nc): per bucket
+// [b 2^21, (b+1) 2^21) of rand, n_lo = #{k : thr[k] <= b 2^21} and 0x80 when
+// more than two thresholds lie strictly inside it
+static void build_buckets(const uint32_t *t0, uint8_t nb[kUtsBuckets]) {
+    for (int b = 0; b < kUtsBuckets; ++b) {
+        const uint64_t lo = (uint64_t)b << kUtsBucketShift, hi = (uint64_t)(b + 1) << kUtsBucketShift;
+        int nlo = 0, inside = 0;
+        for (int k = 1; k <= 100; ++k) {
+            nlo += t0[k] <= lo;
+            inside += t0[k] > lo && t0[k] < hi;
+        }
+        nb[b] = (uint8_t)(nlo | (inside > 2 ? 0x80 : 0));
+    }
+}
+
+// the device lookup of uts_nc<kUtsGeoFixed> (below the depth cut), on the
+// host: bucket byte, two compares, binary search in a dense bucket
+static int bucket_nc(const uint32_t *t0, const uint8_t *nb, uint32_t r) {
+    const uint32_t e = nb[r >> kUtsBucketShift], nlo = e & 0x7fu;
+    uint32_t n = nlo + (t0[nlo + 1] <= r ? 1u : 0u) + (t0[nlo + 2] <= r ? 1u : 0u);
+    if (e & 0x80u) {
+        int lo = (int)nlo, hi = 100;
+        for (int s = 0; s < 7; ++s) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (lo < hi) {
+                if (t0[mid] <= r) lo = mid;
+                else hi = mid - 1;
+            }
+        }
+        n = (uint32_t)lo;
+    }
+    return (int)n;
+}
+
 static int host_nc(const hclib_hip_uts_params_t &p, const UtsTables &T, int d, uint32_t r) {
     int ri = d < (int)T.rules.size() ? d : (int)T.rules.size() - 1;
     int4 rule = T.rules[ri];
@@ -533,6 +567,53 @@ extern "C" int hclib_hip_uts_num_children_host(const hclib_hip_uts_params_t *par
     }
     if (height == 0) return T.root_nc;
     return host_nc(*params, T, height, st[4] & 0x7fffffffu);
+}
+
+// Host check of the bucketed numChildren lookup (no GPU needed): for the
+// tree's first threshold table, the bucket method against the exact count
+// #{k : thr[k] <= r} at every threshold +-3, every bucket edge +-1 and
+// `nrandom` splitmix values of rand. Returns the mismatches (0) or a negative
+// error; *checked receives the values compared.
+extern "C" int hclib_hip_uts_bucket_check(const hclib_hip_uts_params_t *params, uint64_t nrandom,
+                                          uint64_t *checked) {
+    if (!params) {
+        set_error("hclib_hip_uts_bucket_check: NULL params");
+        return HCLIB_HIP_EINVAL;
+    }
+    UtsTables T;
+    if (build_tables(*params, T) != HCLIB_HIP_OK) return HCLIB_HIP_EINVAL;
+    if (T.thr.size() < 128) {  // no threshold table (BIN or constant rules)
+        if (checked) *checked = 0;
+        return 0;
+    }
+    const uint32_t *t0 = T.thr.data();
+    uint8_t nb[kUtsBuckets];
+    build_buckets(t0, nb);
+    uint64_t n = 0;
+    int bad = 0;
+    auto one = [&](int64_t v) {
+        if (v < 0 || v > 0x7fffffffll) return;
+        const uint32_t r = (uint32_t)v;
+        int exact = 0;
+        for (int k = 1; k <= 100; ++k) exact += t0[k] <= r;
+        bad += bucket_nc(t0, nb, r) != exact;
+        ++n;
+    };
+    for (int k = 1; k <= 100; ++k)
+        if (t0[k] != 0x80000000u)
+            for (int d = -3; d <= 3; ++d) one((int64_t)t0[k] + d);
+    for (int b = 0; b <= kUtsBuckets; ++b)
+        for (int d = -1; d <= 1; ++d) one(((int64_t)b << kUtsBucketShift) + d);
+    uint64_t x = 0x9e3779b97f4a7c15ull;
+    for (uint64_t i = 0; i < nrandom; ++i) {
+        x += 0x9e3779b97f4a7c15ull;
+        uint64_t z = x;
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        one((int64_t)((z ^ (z >> 31)) & 0x7fffffffull));
+    }
+    if (checked) *checked = n;
+    return bad;
 }
 
 extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int shard, int nshards,
@@ -567,22 +648,8 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         char *dp = (char *)tab.dmem;
         HX_HIP(hipMemcpy(dp, tab.T.rules.data(), rb, hipMemcpyHostToDevice));
         HX_HIP(hipMemcpy(dp + ((rb + 255) & ~(size_t)255), tab.T.thr.data(), tb, hipMemcpyHostToDevice));
-        // table 0's bucket bytes (kUtsGeoFixed, uts_nc): per bucket
-        // [b 2^21, (b+1) 2^21) of rand, n_lo = #{k : thr[k] <= b 2^21} and
-        // 0x80 when more than two thresholds lie strictly inside it
         uint8_t nb[kUtsBuckets] = {0};
-        if (tab.T.thr.size() >= 128) {
-            const uint32_t *t0 = tab.T.thr.data();
-            for (int b = 0; b < kUtsBuckets; ++b) {
-                const uint64_t lo = (uint64_t)b << kUtsBucketShift, hi = (uint64_t)(b + 1) << kUtsBucketShift;
-                int nlo = 0, inside = 0;
-                for (int k = 1; k <= 100; ++k) {
-                    nlo += t0[k] <= lo;
-                    inside += t0[k] > lo && t0[k] < hi;
-                }
-                nb[b] = (uint8_t)(nlo | (inside > 2 ? 0x80 : 0));
-            }
-        }
+        if (tab.T.thr.size() >= 128) build_buckets(tab.T.thr.data(), nb);
         HX_HIP(hipMemcpy(dp + ((rb + 255) & ~(size_t)255) + ((tb + 255) & ~(size_t)255), nb, kUtsBuckets,
                          hipMemcpyHostToDevice));
         tab.p = *params;

@@ -294,6 +294,12 @@ int hclib_hip_ipc_close(void *dev_ptr);
  * the device uses (threshold tables built from the reference's libm
  * formula, uts.c:171-274) for an explicit node; lets the CPU tests check
  * the tables against the oracle. st = the 5 big-endian state words. */
+/* Host check (no GPU) of the device's bucketed numChildren lookup for
+ * fixed-shape GEO trees: returns the number of rand values where the bucket
+ * method disagrees with #{k : thr[k] <= rand} (0), checking every threshold
+ * +-3, every bucket edge +-1 and `nrandom` pseudo-random values; *checked =
+ * values compared (0 for trees without a threshold table). */
+int hclib_hip_uts_bucket_check(const hclib_hip_uts_params_t *params, uint64_t nrandom, uint64_t *checked);
 int hclib_hip_uts_num_children_host(const hclib_hip_uts_params_t *params, int height,
                                     const uint32_t st[5]);
 

@@ -57,6 +57,19 @@ def test_uts_device_tables_match_reference_vectors(golden, name):
         assert max(got, 0) == want, (name, st, h, got, nc)
 
 
+@pytest.mark.parametrize("name", ["T1", "T1L", "T1XL", "T2", "T4", "T5", "T2L", "T3L"])
+def test_uts_bucketed_num_children_is_exact(golden, name):
+    """The fixed-shape GEO kernels count a node's children with 1,024 rand
+    buckets and two compares (uts.hip uts_nc<kUtsGeoFixed>); the host mirror
+    of that lookup equals #{k : thr[k] <= rand} at every threshold +-3, every
+    bucket edge +-1 and 2^18 random values, for every published tree's first
+    threshold table (BIN trees have none: nothing to check)."""
+    g = golden("uts_goldens.json")
+    bad, n = H.uts_bucket_check(g["published"][name]["args"], 1 << 18)
+    assert bad == 0, (name, bad, n)
+    assert n > (1 << 18) or name == "T3L"
+
+
 @pytest.mark.parametrize("name", ["T1", "T3", "T3L", "T5"])
 def test_uts_device_root_rule(golden, name):
     from oracle import loader as L
