@@ -1404,7 +1404,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         const bool wg = band_shape && env_int("HCLIB_HIP_SW_DAG_WAVE", 0) == 0;
         hclib_hip_dag_launch_t L;
         if ((rc = hclib_hip_dag_begin((uint32_t)nt, (uint32_t)(3 * nt), 0, nullptr, off.data(), ids.data(), nullptr,
-                                      nullptr, wg ? 1 : wpc, c.spin_ms, &L)))
+                                      nullptr, wg ? env_int("HCLIB_HIP_SW_DAG_WGS_PER_CU", 1) : wpc, c.spin_ms, &L)))
             return fail(rc);
         if (wg) {
             const size_t blds = sw_band_lds_bytes(th / bh) + (4 + 2 * (size_t)th) * 4;  // + kept right columns
