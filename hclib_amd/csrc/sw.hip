@@ -1262,6 +1262,319 @@ __global__ __launch_bounds__(1024) void k_sw_dag_wg(SwCtx c, DagView v) {
     run_dag_group<SwDagWgKind>(c, v, &task_slot);
 }
 
+// ------------------------------------------------ packed-half tile bodies
+// A 256-row tile in ONE wave, two cells per VALU operation (gfx950
+// v_pk_maximum3_f16 / v_pk_add_f16). Inside a tile the G values (G = H + row
+// + col, see sw_tile) are kept relative to the tile's corner,
+// v = G - G(R0, C0). G never decreases along a row or a column and grows by
+// at most 4 per diagonal step, so 0 <= v <= 4 max(di, dj) <= 2048 for tiles
+// of at most 256 x 512 cells (and v - 2 >= -2 for a diagonal plus score):
+// integers every f16 holds exactly, so the packed max/add are exact and the
+// outputs bit-identical to the int32 forms.
+// Lane L holds rows 2L, 2L+1 of the tile's top half in the low halves of
+// lr0 / lr1 and rows 128+2L, 129+2L in the high halves; the bottom half
+// runs 64 steps behind the top (the same anti-diagonal pipeline continued
+// through lane 63 -> lane 0): at step s the low halves compute column
+// x = s - L, the high halves x - 64. The cell above a lane's first row comes
+// from lane L-1 (one DPP wave rotation); lane 0 takes the top row (low
+// half) and lane 63's low row 127 (high half) through one byte permute with
+// a per-lane selector. No masks: a column outside the tile has the "null"
+// code, whose score byte is 0, and the top row is 0 beyond the tile — since
+// G is monotone, max3(left, up, diag + 0) then leaves every row at its left
+// value before the tile and at its right-column value after it.
+typedef _Float16 sw_h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ sw_h2 sw_as_h2(uint32_t v) { return __builtin_bit_cast(sw_h2, v); }
+__device__ __forceinline__ uint32_t sw_as_u(sw_h2 v) { return __builtin_bit_cast(uint32_t, v); }
+// f16 bits of an exact small integer (|v| <= 2048)
+__device__ __forceinline__ uint32_t sw_f16_bits(int v) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)v);
+}
+// the score row of s2 code a as the HIGH bytes of f16 (score + 2 = 4, 0 or -2
+// -> 0x44, 0x00, 0xC0; the low byte of each is 0): byte c for s1 code c + 1
+__device__ __forceinline__ uint32_t sw_pk_row(int a) {
+    return a == 1 ? 0xC000C044u : a == 2 ? 0x00C044C0u : a == 3 ? 0xC044C000u : 0x44C000C0u;
+}
+constexpr uint32_t kSwPkNull = 0x0Cu;  // v_perm selector byte of a constant 0x00
+constexpr int kSwPkTh = 256;            // tile rows the packed body covers
+constexpr int kSwPkMaxTw = 512;         // f16 exactness bound (see above)
+// LDS words of the packed body's arrays for tiles ncols wide: the top row
+// (x < ncols + 196, zeros past the tile) and four copies of the per-column
+// permute selectors (x in [-64, ncols + 200)), copy o at word x + 64 + o
+__host__ __device__ constexpr int sw_pk_topw(int ncols) { return (ncols + 196 + 3) & ~3; }
+__host__ __device__ constexpr int sw_pk_selw(int ncols) { return (ncols + 268 + 3) & ~3; }
+
+struct SwPkTile {
+    int R0, C0, ncols;
+    const int *corner_src;  // H(R0, C0) from memory (agent scope), or null:
+    int corner_val;         //   this value (every v is G - G(R0, C0))
+    const int *hin;       // top row H (null: the boundary row, R0 == 0)
+    const int *leftcol;   // H(R0 + 1 + k, C0), k < 256, in global memory, or null:
+    const int *left_lds;  //   in LDS (the workgroup ran the left tile), or null: C0 == 0
+    int *hout;            // bottom row H out
+    int *rightcol;        // right column H out (global), may be null
+    int *rightcol_lds;    // ... and in LDS, may be null
+    int *corner_out;      // H(R0 + 256, C0 + ncols) out, may be null
+    int *corner_out_lds;  // ... and in LDS, may be null
+    int *corner_lds;      // H(R0, C0 + ncols) (the top row's last) into LDS, may be null
+    // diagnostic (HX_DAG_TRACE builds): the task's trace record — [8] inputs
+    // staged, [10] sweep done, [11] outputs issued; null otherwise
+    unsigned long long *trec = nullptr;
+};
+
+// The whole tile by one wave: loads, selector staging, the sweep, outputs.
+// top / sel: this wave's LDS arrays (sw_pk_topw / 4 x sw_pk_selw words,
+// 16-byte aligned). KX = columns per lane (ncols <= 64 KX).
+template <int KX>
+__device__ void sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, int *sel) {
+    const int lane = lane_id();
+    const int ncols = T.ncols, R0 = T.R0, C0 = T.C0;
+    const int topw = sw_pk_topw(ncols), selw = sw_pk_selw(ncols);
+    // --- loads, all issued before any is used, none predicated (a
+    // predicated load becomes a branch that waits for it on its own): the s1
+    // codes first (static input, L2-resident), the rows' s2 codes, the left
+    // column, then the top row and the corner (other tasks' outputs: their
+    // latency overlaps the selector staging below). Unused operands read a
+    // valid word and are discarded.
+    const int xmax = ncols - 1;
+    int code[KX];
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+        const int x = lane + 64 * k;
+        code[k] = (int)c.s1[C0 + (x < ncols ? x : xmax)];
+    }
+    int rowq[4];  // matrix rows of lo q0, lo q1, hi q0, hi q1
+    rowq[0] = R0 + 1 + 2 * lane;
+    rowq[1] = rowq[0] + 1;
+    rowq[2] = rowq[0] + 128;
+    rowq[3] = rowq[1] + 128;
+    int s2c[4], lg[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s2c[q] = c.s2[rowq[q] - 1];
+    const bool lglob = T.leftcol != nullptr;
+    const int *lsrc = lglob ? T.leftcol : T.hout;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lg[q] = ld_agent(&lsrc[lglob ? rowq[q] - R0 - 1 : 0]);
+    int th_[KX];
+    const int *hsrc = T.hin ? T.hin : T.hout;
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+        const int x = lane + 64 * k;
+        th_[k] = ld_agent(&hsrc[T.hin ? (x < ncols ? x : xmax) : 0]);
+    }
+    const int cget = ld_agent(T.corner_src ? T.corner_src : T.hout);
+#pragma unroll
+    for (int k = 0; k < KX; ++k)
+        if (lane + 64 * k >= ncols) code[k] = (int)kSwPkNull;
+        else code[k] -= 1;
+    int lh[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        lh[q] = T.left_lds ? *((const lds_i32 *)T.left_lds + (rowq[q] - R0 - 1)) : (lglob ? lg[q] : -rowq[q]);
+    // --- selectors: word x = [hi: 4 + code(x - 64) | null][0x0C][lo: code(x)][0x0C]
+    // (the score bytes of the low and the high half: S1 = the low rows' row,
+    // S0 = the high rows'), staged for x in [-64, ncols + 200) in four copies
+    // so that lane L reads four consecutive columns from copy L & 3 aligned
+    auto selword = [](int lo, int hi) {
+        const uint32_t hs = hi == (int)kSwPkNull ? kSwPkNull : (uint32_t)(4 + hi);
+        return kSwPkNull | ((uint32_t)lo << 8) | (kSwPkNull << 16) | (hs << 24);
+    };
+    // x = lane + 64 k - 64 for k = 0 .. KX + 5: lo code = code[k - 1], hi = code[k - 2]
+#pragma unroll
+    for (int k = 0; k < KX + 6; ++k) {
+        const int x = lane + 64 * k - 64;
+        if (x < ncols + 200) {
+            const int lo = (k >= 1 && k - 1 < KX) ? code[k - 1] : (int)kSwPkNull;
+            const int hi = (k >= 2 && k - 2 < KX) ? code[k - 2] : (int)kSwPkNull;
+            const uint32_t w = selword(lo, hi);
+#pragma unroll
+            for (int o = 0; o < 4; ++o) sel[o * selw + x + 64 + o] = (int)w;
+        }
+    }
+    // --- the rows' score tables and the left column as packed v
+    const int base = (T.corner_src ? cget : T.corner_val) + R0 + C0;  // G(R0, C0)
+    const uint32_t mlo0 = sw_pk_row(s2c[0]), mlo1 = sw_pk_row(s2c[1]);
+    const uint32_t mhi0 = sw_pk_row(s2c[2]), mhi1 = sw_pk_row(s2c[3]);
+    uint32_t l16[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) l16[q] = sw_f16_bits(lh[q] + rowq[q] + C0 - base);
+    sw_h2 lr0 = sw_as_h2(l16[0] | (l16[2] << 16)), lr1 = sw_as_h2(l16[1] | (l16[3] << 16));
+    // --- the top row as v (f16 in the low half), 0 past the tile
+#pragma unroll
+    for (int k = 0; k < KX + 4; ++k) {
+        const int x = lane + 64 * k;
+        if (x < topw) {
+            int v = 0;
+            if (k < KX && x < ncols) v = T.hin ? th_[k] + R0 + (C0 + 1 + x) - base : -base;
+            top[x] = (int)sw_f16_bits(v);
+        }
+    }
+    if (T.corner_lds) {
+        // H(R0, C0 + ncols): the up tile's last bottom value (or the boundary)
+        const int xl = ncols - 1;
+        if ((xl & 63) == lane) {
+            int h = -(C0 + ncols);
+#pragma unroll
+            for (int k = 0; k < KX; ++k)
+                if (k == (xl >> 6) && T.hin) h = th_[k];
+            *T.corner_lds = h;
+        }
+    }
+    auto tstamp = [&](int k) {
+        if (HX_DAG_TRACE && T.trec && lane == 0) T.trec[k] = __builtin_amdgcn_s_memrealtime();
+    };
+    tstamp(8);
+    // --- the sweep: S = ncols + 127 steps in chunks of 64; the tile's bottom
+    // row (lane 63's high row 255) leaves in pairs of steps, one DPP shift
+    // per pair (see the chunk's end)
+    const uint32_t selU = lane == 0 ? 0x05040100u : 0x07060504u;
+    // the up value of step -1 (lane 0's top-row input: the corner, v = 0)
+    sw_h2 upp = sw_as_h2(__builtin_amdgcn_perm((uint32_t)__builtin_amdgcn_mov_dpp((int)sw_as_u(lr1), 0x13C, 0xf, 0xf, false),
+                                               0u, selU));
+    const int *selp = sel + (lane & 3) * selw + 64 + (lane & 3) - lane;  // + s: column s - lane, aligned
+    const int nsteps = ncols + 127;
+    const int Rb = R0 + kSwPkTh;  // the bottom row's matrix row
+    for (int s0 = 0; s0 < nsteps; s0 += 64) {
+        uint32_t acc = 0;
+        int4 tn = *(const int4 *)(top + s0), sn = *(const int4 *)(selp + s0);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int4 tc = tn, sc4 = sn;
+            if (g < 15) {
+                tn = *(const int4 *)(top + s0 + 4 * g + 4);
+                sn = *(const int4 *)(selp + s0 + 4 * g + 4);
+            }
+            const int tv[4] = {tc.x, tc.y, tc.z, tc.w};
+            const int sv[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                // wave_ror:1 (every lane has a source: no old value to keep)
+                const uint32_t rot = (uint32_t)__builtin_amdgcn_mov_dpp((int)sw_as_u(lr1), 0x13C, 0xf, 0xf, false);
+                const sw_h2 up = sw_as_h2(__builtin_amdgcn_perm(rot, (uint32_t)tv[jj], selU));
+                const sw_h2 sc0 = sw_as_h2(__builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv[jj]));
+                const sw_h2 sc1 = sw_as_h2(__builtin_amdgcn_perm(mhi1, mlo1, (uint32_t)sv[jj]));
+                const sw_h2 h0 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(lr0, up), upp + sc0);
+                const sw_h2 h1 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(lr1, h0), lr0 + sc1);
+                if (jj & 1) {
+                    // two steps' bottom-row values (lane 63's high halves) as one
+                    // word, shifted down a lane (wave_shl:1; lane 63 keeps the pair)
+                    const uint32_t pair = __builtin_amdgcn_perm(sw_as_u(h1), sw_as_u(lr1), 0x07060302u);
+                    acc = (uint32_t)__builtin_amdgcn_update_dpp((int)pair, (int)acc, 0x130, 0xf, 0xf, false);
+                }
+                upp = up;
+                lr0 = h0;
+                lr1 = h1;
+            }
+        }
+        // lanes 32 + p hold steps s0 + 2p (low half) and s0 + 2p + 1 (high)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int x = s0 + 2 * (lane - 32) + e - 127;  // the bottom row's column
+            if (lane >= 32 && x >= 0 && x < ncols) {
+                const sw_h2 pv = sw_as_h2(acc);
+                const int h = (int)(float)(e ? pv.y : pv.x) + base - Rb - (C0 + 1 + x);
+                st_agent(&T.hout[x], h);
+                if (x == ncols - 1) {
+                    if (T.corner_out) st_agent(T.corner_out, h);
+                    if (T.corner_out_lds) *T.corner_out_lds = h;
+                }
+            }
+        }
+    }
+    tstamp(10);
+    // --- the right column: every row's value at its last column
+    const int Cr = C0 + ncols;
+    int rv[4];
+    rv[0] = (int)(float)lr0.x + base - rowq[0] - Cr;
+    rv[1] = (int)(float)lr1.x + base - rowq[1] - Cr;
+    rv[2] = (int)(float)lr0.y + base - rowq[2] - Cr;
+    rv[3] = (int)(float)lr1.y + base - rowq[3] - Cr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int k = rowq[q] - R0 - 1;
+        if (T.rightcol) st_agent(&T.rightcol[k], rv[q]);
+        if (T.rightcol_lds) T.rightcol_lds[k] = rv[q];
+    }
+    tstamp(11);
+    tstamp(9);
+}
+
+// The promise DAG with the packed body: workgroups of two waves, wave 0 the
+// tile (and the tickets), wave 1 run_dag_group's helper (waiter prefetch,
+// datums). LDS: top | sel x 4 | right columns [2][256] | misc words.
+struct SwDagPkKind {
+    using Ctx = SwCtx;
+    static constexpr bool kSc1Payload = true;  // tile inputs/outputs move by ld_agent / st_agent
+    __device__ static int *misc_of(const SwCtx &c) {
+        extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+        return sw_lds + sw_pk_topw(c.tw) + 4 * sw_pk_selw(c.tw) + 2 * kSwPkTh;
+    }
+    // misc: [0] the workgroup's last tile, [1..2] kept corners by parity,
+    // [3] the corner datum, [4] the finished tile + 1 (wave 1 waits on it)
+    __device__ static bool run_group(const SwCtx &c, uint32_t t, const uint32_t *, int wave) {
+        extern __shared__ __attribute__((aligned(16))) int sw_lds[];
+        int *misc = misc_of(c);
+        if (wave != 0) {
+            // the helper returns once the tile's LDS outputs (the datum) exist
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t n = 1; lds_flag_ld(&misc[4]) != (int)t + 1; ++n) {
+                __builtin_amdgcn_s_sleep(1);
+                if ((n & 255) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
+                    if (lane_id() == 0) dev_error(c.err, kErrSpinTimeout);
+                    return false;
+                }
+            }
+            return true;
+        }
+        int *top = sw_lds, *sel = top + sw_pk_topw(c.tw), *right_keep = sel + 4 * sw_pk_selw(c.tw);
+        const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
+        const bool from_lds = j > 0 && misc[0] == (int)t - 1;
+        SwPkTile T;
+        T.R0 = i * kSwPkTh;
+        T.C0 = j * c.tw;
+        T.ncols = c.tw;
+        T.corner_src = (T.R0 == 0 || j == 0 || from_lds) ? nullptr : &c.corner[t - (uint32_t)c.ntw - 1];
+        T.corner_val = T.R0 == 0 ? -T.C0 : (j == 0 ? -T.R0 : (from_lds ? misc[1 + ((t - 1) & 1)] : 0));
+        T.hin = i > 0 ? c.bottom + (size_t)(t - (uint32_t)c.ntw) * c.tw : nullptr;
+        T.left_lds = j > 0 && from_lds ? right_keep + ((t - 1) & 1) * kSwPkTh : nullptr;
+        T.leftcol = j > 0 && !from_lds ? c.right + (size_t)(t - 1) * kSwPkTh : nullptr;
+        T.hout = c.bottom + (size_t)t * c.tw;
+        T.rightcol = c.right + (size_t)t * kSwPkTh;
+        T.rightcol_lds = right_keep + (t & 1) * kSwPkTh;
+        T.corner_out = c.corner + t;
+        T.corner_out_lds = &misc[3];
+        T.corner_lds = &misc[1 + (t & 1)];
+        T.trec = HX_DAG_TRACE && c.dtrace ? c.dtrace + (size_t)t * kDagTraceWords : nullptr;
+        if (c.tw <= 256) sw_pk_tile<4>(c, T, top, sel);
+        else sw_pk_tile<8>(c, T, top, sel);
+        if (lane_id() == 0) lds_flag_st(&misc[4], (int)t + 1);
+        return true;
+    }
+    __device__ static void after_body(const SwCtx &c, uint32_t t) {
+        if (threadIdx.x == 0) misc_of(c)[0] = (int)t;
+    }
+    static constexpr int kPutN = 3;
+    __device__ static void promises(const SwCtx &, uint32_t t, uint32_t (&p)[3]) {
+        p[0] = 3u * t + 0u;
+        p[1] = 3u * t + 1u;
+        p[2] = 3u * t + 2u;
+    }
+    __device__ static void datums(const SwCtx &c, uint32_t, unsigned long long (&d)[3]) {
+        d[0] = 0ull;
+        d[1] = 0ull;
+        d[2] = (unsigned long long)(uint32_t)misc_of(c)[3];  // c.corner[t] (:224-226)
+    }
+};
+
+__global__ __launch_bounds__(128) void k_sw_dag_pk(SwCtx c, DagView v) {
+    int *misc = SwDagPkKind::misc_of(c);
+    if (threadIdx.x == 0) {
+        misc[0] = -2;  // no tile yet (run_dag_group's first barrier orders these)
+        misc[4] = 0;
+    }
+    run_dag_group<SwDagPkKind>(c, v, nullptr);
+}
+inline size_t sw_pk_lds_bytes(int tw) { return (size_t)(sw_pk_topw(tw) + 4 * sw_pk_selw(tw) + 2 * kSwPkTh + 8) * 4; }
+
 __global__ void k_sw_init(uint32_t *deps, uint32_t *ready, int ntw, int nth) {
     const uint32_t n = (uint32_t)(ntw * nth);
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
@@ -1402,11 +1715,22 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         // tile tasks on workgroups of th / 64 + 2 waves where the band
         // kernel applies (HCLIB_HIP_SW_DAG_WAVE=1: one wave per tile)
         const bool wg = band_shape && env_int("HCLIB_HIP_SW_DAG_WAVE", 0) == 0;
+        // 256-row tiles at most 512 wide: the packed-half body, one wave per
+        // tile (HCLIB_HIP_SW_PK=0: the band forms above)
+        const bool pk = th == kSwPkTh && tw <= kSwPkMaxTw && env_int("HCLIB_HIP_SW_PK", 1) != 0;
         hclib_hip_dag_launch_t L;
         if ((rc = hclib_hip_dag_begin((uint32_t)nt, (uint32_t)(3 * nt), 0, nullptr, off.data(), ids.data(), nullptr,
-                                      nullptr, wg ? env_int("HCLIB_HIP_SW_DAG_WGS_PER_CU", 1) : wpc, c.spin_ms, &L)))
+                                      nullptr, pk ? env_int("HCLIB_HIP_SW_PK_WGS_PER_CU", 1)
+                                                  : (wg ? env_int("HCLIB_HIP_SW_DAG_WGS_PER_CU", 1) : wpc),
+                                      c.spin_ms, &L)))
             return fail(rc);
-        if (wg) {
+        if (pk) {
+            const size_t plds = sw_pk_lds_bytes(tw);
+            c.dtrace = ((const DagView *)L.view)->trace;
+            if (plds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_pk,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
+            hipLaunchKernelGGL(k_sw_dag_pk, dim3(L.grid), dim3(128), plds, m.stream, c, *(const DagView *)L.view);
+        } else if (wg) {
             const size_t blds = sw_band_lds_bytes(th / bh) + (4 + 2 * (size_t)th) * 4;  // + kept right columns
             if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_wg,
                                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);

@@ -294,6 +294,30 @@ def test_sw_64k_golden_on_generic_promise_dag(golden, monkeypatch):
     assert st["tiles"] == 65536
 
 
+@pytest.mark.parametrize("tw", [1, 30, 63, 64, 65, 100, 256, 300, 511, 512])
+def test_sw_dag_packed_half_tiles(tw, monkeypatch):
+    """256-row tiles at most 512 wide run the promise DAG's packed-half body
+    (one wave per tile, two cells per v_pk_maximum3_f16, values relative to
+    each tile's corner): the oracle's score on ragged random inputs and on
+    all-match inputs (+4 on every diagonal, so the relative values reach the
+    f16-exact bound of 2048 at tw = 512), and the int32 band form's
+    (HCLIB_HIP_SW_PK=0) on the same inputs."""
+    monkeypatch.setenv("HCLIB_HIP_SW_SCHED", "dag")
+    rng = np.random.default_rng(tw)
+    n1 = tw * (3 if tw >= 64 else 17) + tw // 3
+    n2 = 256 * 3 + 100
+    cases = [(rng.integers(1, 5, n1), rng.integers(1, 5, n2)), (np.full(n1, 1), np.full(n2, 1)),
+             (np.full(n1, 2), rng.integers(1, 5, n2))]
+    for a, b in cases:
+        a, b = a.astype(np.int8).tobytes(), b.astype(np.int8).tobytes()
+        want = L.sw_score(a, b, tw, 256)
+        score, st = H.sw(a, b, tw, 256)
+        assert score == want and st["tiles"] == (n1 // tw) * 3, (tw, score, want)
+        monkeypatch.setenv("HCLIB_HIP_SW_PK", "0")
+        assert H.sw(a, b, tw, 256)[0] == want
+        monkeypatch.delenv("HCLIB_HIP_SW_PK")
+
+
 def test_sw_random_vs_oracle():
     rng = np.random.default_rng(5)
     for (n1, n2, tw, th) in [(300, 200, 17, 13), (1000, 777, 64, 300), (513, 1025, 256, 64)]:
