@@ -1321,56 +1321,70 @@ struct SwPkTile {
     unsigned long long *trec = nullptr;
 };
 
-// The whole tile by one wave: loads, selector staging, the sweep, outputs.
-// top / sel: this wave's LDS arrays (sw_pk_topw / 4 x sw_pk_selw words,
-// 16-byte aligned). KX = columns per lane (ncols <= 64 KX).
+// The tile as two waves of one workgroup: the sweep wave (wave 0) runs the
+// dependent chain; the score wave (wave 1) feeds it the packed score words
+// of every step through an LDS ring, so the sweep issues no score lookups.
+// One wave issues at most one VALU operation per ~5 cycles whatever the rest
+// of the CU does (profiles/r03/ub_valu.log), so a step's cost is its
+// instruction count: moving the two lookups (v_perm) and the selector loads
+// to a second wave leaves the sweep rot + up + 2 adds + 2 max3 + half a
+// gather and half a ring load per step.
+// Ring: kSwPkSlots chunks of 64 steps; a chunk is 32 step pairs x 64 lanes of
+// uint4 {sc0(2p), sc1(2p), sc0(2p+1), sc1(2p+1)}. misc[5] = chunks written,
+// misc[6] = chunks read (both reset between tiles).
+constexpr int kSwPkSlots = 2;
+// Timing experiments (diagnostic builds only, results wrong by design):
+// 1 = the score wave computes chunk 0 only and then just publishes the rest,
+// 2 = the sweep wave reads no ring (constant scores)
+#ifndef HX_SW_PK_EXP
+#define HX_SW_PK_EXP 0
+#endif
+constexpr int kSwPkRingU4 = kSwPkSlots * 32 * 64;  // uint4 entries
+// LDS: ring | top | sel x 4 | right columns [2][256] | misc[8] | score rows [4][64]
+__host__ __device__ constexpr int sw_pk_lds_words(int tw) {
+    return kSwPkRingU4 * 4 + sw_pk_topw(tw) + 4 * sw_pk_selw(tw) + 2 * kSwPkTh + 8 + 256;
+}
+inline size_t sw_pk_lds_bytes(int tw) { return (size_t)sw_pk_lds_words(tw) * 4; }
+
+// wait until an LDS counter reaches `want` (bounded; device error on timeout)
+__device__ __forceinline__ bool sw_pk_wait(const SwCtx &c, const int *flag, int want) {
+    if (lds_flag_ld(flag) >= want) return true;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t n = 1; lds_flag_ld(flag) < want; ++n) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((n & 255) == 0) {
+            if (ld_agent(c.err)) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
+                if (lane_id() == 0) dev_error(c.err, kErrSpinTimeout);
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
+// The score wave's staging for a tile: its s1 codes as permute selectors
+// (sel) and this lane's four score rows (tbl[q * 64 + lane]). Run for the
+// tile itself, or ahead of time for the right neighbour (the tile the
+// workgroup keeps when its own put releases it) while the sweep still runs.
 template <int KX>
-__device__ void sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, int *sel) {
+__device__ void sw_pk_stage(const SwCtx &c, int R0, int C0, int ncols, int *sel, int *tbl) {
     const int lane = lane_id();
-    const int ncols = T.ncols, R0 = T.R0, C0 = T.C0;
-    const int topw = sw_pk_topw(ncols), selw = sw_pk_selw(ncols);
-    // --- loads, all issued before any is used, none predicated (a
-    // predicated load becomes a branch that waits for it on its own): the s1
-    // codes first (static input, L2-resident), the rows' s2 codes, the left
-    // column, then the top row and the corner (other tasks' outputs: their
-    // latency overlaps the selector staging below). Unused operands read a
-    // valid word and are discarded.
-    const int xmax = ncols - 1;
+    const int selw = sw_pk_selw(ncols), xmax = ncols - 1;
     int code[KX];
 #pragma unroll
     for (int k = 0; k < KX; ++k) {
         const int x = lane + 64 * k;
         code[k] = (int)c.s1[C0 + (x < ncols ? x : xmax)];
     }
-    int rowq[4];  // matrix rows of lo q0, lo q1, hi q0, hi q1
-    rowq[0] = R0 + 1 + 2 * lane;
-    rowq[1] = rowq[0] + 1;
-    rowq[2] = rowq[0] + 128;
-    rowq[3] = rowq[1] + 128;
-    int s2c[4], lg[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) s2c[q] = c.s2[rowq[q] - 1];
-    const bool lglob = T.leftcol != nullptr;
-    const int *lsrc = lglob ? T.leftcol : T.hout;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) lg[q] = ld_agent(&lsrc[lglob ? rowq[q] - R0 - 1 : 0]);
-    int th_[KX];
-    const int *hsrc = T.hin ? T.hin : T.hout;
-#pragma unroll
-    for (int k = 0; k < KX; ++k) {
-        const int x = lane + 64 * k;
-        th_[k] = ld_agent(&hsrc[T.hin ? (x < ncols ? x : xmax) : 0]);
-    }
-    const int cget = ld_agent(T.corner_src ? T.corner_src : T.hout);
+    // this lane's rows: lo q0, lo q1, hi q0, hi q1 (as the sweep wave's)
+    const int r0 = R0 + 1 + 2 * lane;
+    const int s2a = c.s2[r0 - 1], s2b = c.s2[r0], s2c = c.s2[r0 + 127], s2d = c.s2[r0 + 128];
 #pragma unroll
     for (int k = 0; k < KX; ++k)
         if (lane + 64 * k >= ncols) code[k] = (int)kSwPkNull;
         else code[k] -= 1;
-    int lh[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        lh[q] = T.left_lds ? *((const lds_i32 *)T.left_lds + (rowq[q] - R0 - 1)) : (lglob ? lg[q] : -rowq[q]);
-    // --- selectors: word x = [hi: 4 + code(x - 64) | null][0x0C][lo: code(x)][0x0C]
+    // selectors: word x = [hi: 4 + code(x - 64) | null][0x0C][lo: code(x)][0x0C]
     // (the score bytes of the low and the high half: S1 = the low rows' row,
     // S0 = the high rows'), staged for x in [-64, ncols + 200) in four copies
     // so that lane L reads four consecutive columns from copy L & 3 aligned
@@ -1390,10 +1404,78 @@ __device__ void sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, int *sel
             for (int o = 0; o < 4; ++o) sel[o * selw + x + 64 + o] = (int)w;
         }
     }
-    // --- the rows' score tables and the left column as packed v
+    tbl[lane] = (int)sw_pk_row(s2a);
+    tbl[64 + lane] = (int)sw_pk_row(s2b);
+    tbl[128 + lane] = (int)sw_pk_row(s2c);
+    tbl[192 + lane] = (int)sw_pk_row(s2d);
+}
+
+// The score wave: every chunk's scores from the staged selectors and rows.
+__device__ bool sw_pk_scores(const SwCtx &c, int ncols, uint4 *ring, const int *sel, const int *tbl, int *misc) {
+    const int lane = lane_id();
+    const int selw = sw_pk_selw(ncols);
+    const uint32_t mlo0 = (uint32_t)tbl[lane], mlo1 = (uint32_t)tbl[64 + lane];
+    const uint32_t mhi0 = (uint32_t)tbl[128 + lane], mhi1 = (uint32_t)tbl[192 + lane];
+    const int *selp = sel + (lane & 3) * selw + 64 + (lane & 3) - lane;  // + s: column s - lane, aligned
+    const int nch = (ncols + 127 + 63) / 64;
+    for (int k = 0; k < nch; ++k) {
+        if (k >= kSwPkSlots && !sw_pk_wait(c, &misc[6], k + 1 - kSwPkSlots)) return false;
+        uint4 *dst = ring + (size_t)((k % kSwPkSlots) * 32) * 64 + lane;
+        const int *sp = selp + 64 * k;
+#pragma unroll
+        for (int g = 0; g < 16 && (HX_SW_PK_EXP != 1 || k == 0); ++g) {
+            const int4 sv = *(const int4 *)(sp + 4 * g);
+            dst[(2 * g) * 64] = make_uint4(__builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv.x),
+                                           __builtin_amdgcn_perm(mhi1, mlo1, (uint32_t)sv.x),
+                                           __builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv.y),
+                                           __builtin_amdgcn_perm(mhi1, mlo1, (uint32_t)sv.y));
+            dst[(2 * g + 1) * 64] = make_uint4(__builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv.z),
+                                               __builtin_amdgcn_perm(mhi1, mlo1, (uint32_t)sv.z),
+                                               __builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv.w),
+                                               __builtin_amdgcn_perm(mhi1, mlo1, (uint32_t)sv.w));
+        }
+        if (lane == 0) lds_flag_st(&misc[5], k + 1);
+    }
+    return true;
+}
+
+// The sweep wave: the tile's inputs, the sweep, its outputs. top: this
+// workgroup's top-row array (sw_pk_topw words, 16-byte aligned). KX =
+// columns per lane (ncols <= 64 KX).
+template <int KX>
+__device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const uint4 *ring, int *misc) {
+    const int lane = lane_id();
+    const int ncols = T.ncols, R0 = T.R0, C0 = T.C0;
+    const int topw = sw_pk_topw(ncols);
+    // --- loads, all issued before any is used, none predicated (a
+    // predicated load becomes a branch that waits for it on its own): the left
+    // column, the top row and the corner (other tasks' outputs). Unused
+    // operands read a valid word and are discarded.
+    const int xmax = ncols - 1;
+    int rowq[4];  // matrix rows of lo q0, lo q1, hi q0, hi q1
+    rowq[0] = R0 + 1 + 2 * lane;
+    rowq[1] = rowq[0] + 1;
+    rowq[2] = rowq[0] + 128;
+    rowq[3] = rowq[1] + 128;
+    int lg[4];
+    const bool lglob = T.leftcol != nullptr;
+    const int *lsrc = lglob ? T.leftcol : T.hout;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lg[q] = ld_agent(&lsrc[lglob ? rowq[q] - R0 - 1 : 0]);
+    int th_[KX];
+    const int *hsrc = T.hin ? T.hin : T.hout;
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+        const int x = lane + 64 * k;
+        th_[k] = ld_agent(&hsrc[T.hin ? (x < ncols ? x : xmax) : 0]);
+    }
+    const int cget = ld_agent(T.corner_src ? T.corner_src : T.hout);
+    int lh[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        lh[q] = T.left_lds ? *((const lds_i32 *)T.left_lds + (rowq[q] - R0 - 1)) : (lglob ? lg[q] : -rowq[q]);
+    // --- the left column as packed v
     const int base = (T.corner_src ? cget : T.corner_val) + R0 + C0;  // G(R0, C0)
-    const uint32_t mlo0 = sw_pk_row(s2c[0]), mlo1 = sw_pk_row(s2c[1]);
-    const uint32_t mhi0 = sw_pk_row(s2c[2]), mhi1 = sw_pk_row(s2c[3]);
     uint32_t l16[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) l16[q] = sw_f16_bits(lh[q] + rowq[q] + C0 - base);
@@ -1430,30 +1512,38 @@ __device__ void sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, int *sel
     // the up value of step -1 (lane 0's top-row input: the corner, v = 0)
     sw_h2 upp = sw_as_h2(__builtin_amdgcn_perm((uint32_t)__builtin_amdgcn_mov_dpp((int)sw_as_u(lr1), 0x13C, 0xf, 0xf, false),
                                                0u, selU));
-    const int *selp = sel + (lane & 3) * selw + 64 + (lane & 3) - lane;  // + s: column s - lane, aligned
     const int nsteps = ncols + 127;
     const int Rb = R0 + kSwPkTh;  // the bottom row's matrix row
-    for (int s0 = 0; s0 < nsteps; s0 += 64) {
+    for (int s0 = 0, k = 0; s0 < nsteps; s0 += 64, ++k) {
+        if (!sw_pk_wait(c, &misc[5], k + 1)) return false;
+        if (k == 0) tstamp(12);  // the first chunk's scores are there
+        const uint4 *src = ring + (size_t)((k % kSwPkSlots) * 32) * 64 + lane;
         uint32_t acc = 0;
-        int4 tn = *(const int4 *)(top + s0), sn = *(const int4 *)(selp + s0);
+        int4 tn = *(const int4 *)(top + s0);
+        uint4 rn0 = src[0], rn1 = src[64];
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-            const int4 tc = tn, sc4 = sn;
+            const int4 tc = tn;
+            const uint4 r0 = rn0, r1 = rn1;
             if (g < 15) {
                 tn = *(const int4 *)(top + s0 + 4 * g + 4);
-                sn = *(const int4 *)(selp + s0 + 4 * g + 4);
+                if (HX_SW_PK_EXP == 2) {
+                    rn0 = make_uint4(g, 2 * g, g, 2 * g);
+                    rn1 = make_uint4(3 * g, g, 3 * g, g);
+                } else {
+                    rn0 = src[(2 * g + 2) * 64];
+                    rn1 = src[(2 * g + 3) * 64];
+                }
             }
             const int tv[4] = {tc.x, tc.y, tc.z, tc.w};
-            const int sv[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+            const uint32_t s0v[4] = {r0.x, r0.z, r1.x, r1.z}, s1v[4] = {r0.y, r0.w, r1.y, r1.w};
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
                 // wave_ror:1 (every lane has a source: no old value to keep)
                 const uint32_t rot = (uint32_t)__builtin_amdgcn_mov_dpp((int)sw_as_u(lr1), 0x13C, 0xf, 0xf, false);
                 const sw_h2 up = sw_as_h2(__builtin_amdgcn_perm(rot, (uint32_t)tv[jj], selU));
-                const sw_h2 sc0 = sw_as_h2(__builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv[jj]));
-                const sw_h2 sc1 = sw_as_h2(__builtin_amdgcn_perm(mhi1, mlo1, (uint32_t)sv[jj]));
-                const sw_h2 h0 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(lr0, up), upp + sc0);
-                const sw_h2 h1 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(lr1, h0), lr0 + sc1);
+                const sw_h2 h0 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(lr0, up), upp + sw_as_h2(s0v[jj]));
+                const sw_h2 h1 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(lr1, h0), lr0 + sw_as_h2(s1v[jj]));
                 if (jj & 1) {
                     // two steps' bottom-row values (lane 63's high halves) as one
                     // word, shifted down a lane (wave_shl:1; lane 63 keeps the pair)
@@ -1465,6 +1555,7 @@ __device__ void sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, int *sel
                 lr1 = h1;
             }
         }
+        if (lane == 0) lds_flag_st(&misc[6], k + 1);  // the chunk's ring slot is free
         // lanes 32 + p hold steps s0 + 2p (low half) and s0 + 2p + 1 (high)
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -1496,37 +1587,52 @@ __device__ void sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, int *sel
     }
     tstamp(11);
     tstamp(9);
+    return true;
 }
 
-// The promise DAG with the packed body: workgroups of two waves, wave 0 the
-// tile (and the tickets), wave 1 run_dag_group's helper (waiter prefetch,
-// datums). LDS: top | sel x 4 | right columns [2][256] | misc words.
+// The promise DAG with the packed body: workgroups of three waves, wave 0
+// the sweep (and the tickets), wave 1 the scores, wave 2 run_dag_group's
+// helper (waiter prefetch, datums: its global round trips stay off the
+// score wave's start).
 struct SwDagPkKind {
     using Ctx = SwCtx;
     static constexpr bool kSc1Payload = true;  // tile inputs/outputs move by ld_agent / st_agent
     __device__ static int *misc_of(const SwCtx &c) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
-        return sw_lds + sw_pk_topw(c.tw) + 4 * sw_pk_selw(c.tw) + 2 * kSwPkTh;
+        return sw_lds + sw_pk_lds_words(c.tw) - 8 - 256;
     }
     // misc: [0] the workgroup's last tile, [1..2] kept corners by parity,
-    // [3] the corner datum, [4] the finished tile + 1 (wave 1 waits on it)
+    // [3] the corner datum, [4] the finished tile + 1 (wave 1 waits on it),
+    // [5] / [6] score chunks written / read, [7] the tile whose selectors and
+    // score rows are staged (misc + 8: the rows, [4][64])
     __device__ static bool run_group(const SwCtx &c, uint32_t t, const uint32_t *, int wave) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
         int *misc = misc_of(c);
-        if (wave != 0) {
-            // the helper returns once the tile's LDS outputs (the datum) exist
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            for (uint32_t n = 1; lds_flag_ld(&misc[4]) != (int)t + 1; ++n) {
-                __builtin_amdgcn_s_sleep(1);
-                if ((n & 255) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
-                    if (lane_id() == 0) dev_error(c.err, kErrSpinTimeout);
-                    return false;
-                }
+        uint4 *ring = (uint4 *)sw_lds;
+        int *top = sw_lds + kSwPkRingU4 * 4, *sel = top + sw_pk_topw(c.tw), *right_keep = sel + 4 * sw_pk_selw(c.tw);
+        const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
+        if (wave == 2) {
+            // run_dag_group's helper (the workgroup's last wave): returns once
+            // the tile's LDS outputs (the corner datum) exist
+            return sw_pk_wait(c, &misc[4], (int)t + 1);
+        }
+        if (wave == 1) {
+            int *tbl = misc + 8;
+            // staged ahead (misc[7] == t) or now
+            if (misc[7] != (int)t) {
+                if (c.tw <= 256) sw_pk_stage<4>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl);
+                else sw_pk_stage<8>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl);
             }
+            if (!sw_pk_scores(c, c.tw, ring, sel, tbl, misc)) return false;
+            // while the sweep runs: stage the right neighbour
+            const bool next = j + 1 < c.ntw;
+            if (next) {
+                if (c.tw <= 256) sw_pk_stage<4>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl);
+                else sw_pk_stage<8>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl);
+            }
+            if (lane_id() == 0) misc[7] = next ? (int)t + 1 : -1;
             return true;
         }
-        int *top = sw_lds, *sel = top + sw_pk_topw(c.tw), *right_keep = sel + 4 * sw_pk_selw(c.tw);
-        const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
         const bool from_lds = j > 0 && misc[0] == (int)t - 1;
         SwPkTile T;
         T.R0 = i * kSwPkTh;
@@ -1544,13 +1650,19 @@ struct SwDagPkKind {
         T.corner_out_lds = &misc[3];
         T.corner_lds = &misc[1 + (t & 1)];
         T.trec = HX_DAG_TRACE && c.dtrace ? c.dtrace + (size_t)t * kDagTraceWords : nullptr;
-        if (c.tw <= 256) sw_pk_tile<4>(c, T, top, sel);
-        else sw_pk_tile<8>(c, T, top, sel);
-        if (lane_id() == 0) lds_flag_st(&misc[4], (int)t + 1);
-        return true;
+        const bool ok = c.tw <= 256 ? sw_pk_tile<4>(c, T, top, ring, misc) : sw_pk_tile<8>(c, T, top, ring, misc);
+        if (ok && lane_id() == 0) lds_flag_st(&misc[4], (int)t + 1);
+        return ok;
     }
+    // between tiles: this tile recorded as the workgroup's last, the score
+    // ring's counters back to 0
     __device__ static void after_body(const SwCtx &c, uint32_t t) {
-        if (threadIdx.x == 0) misc_of(c)[0] = (int)t;
+        if (threadIdx.x == 0) {
+            int *misc = misc_of(c);
+            misc[0] = (int)t;
+            misc[5] = 0;
+            misc[6] = 0;
+        }
     }
     static constexpr int kPutN = 3;
     __device__ static void promises(const SwCtx &, uint32_t t, uint32_t (&p)[3]) {
@@ -1565,15 +1677,17 @@ struct SwDagPkKind {
     }
 };
 
-__global__ __launch_bounds__(128) void k_sw_dag_pk(SwCtx c, DagView v) {
+__global__ __launch_bounds__(192) void k_sw_dag_pk(SwCtx c, DagView v) {
     int *misc = SwDagPkKind::misc_of(c);
     if (threadIdx.x == 0) {
         misc[0] = -2;  // no tile yet (run_dag_group's first barrier orders these)
         misc[4] = 0;
+        misc[5] = 0;
+        misc[6] = 0;
+        misc[7] = -1;  // no tile's scores staged
     }
     run_dag_group<SwDagPkKind>(c, v, nullptr);
 }
-inline size_t sw_pk_lds_bytes(int tw) { return (size_t)(sw_pk_topw(tw) + 4 * sw_pk_selw(tw) + 2 * kSwPkTh + 8) * 4; }
 
 __global__ void k_sw_init(uint32_t *deps, uint32_t *ready, int ntw, int nth) {
     const uint32_t n = (uint32_t)(ntw * nth);
@@ -1729,7 +1843,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
             c.dtrace = ((const DagView *)L.view)->trace;
             if (plds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_pk,
                                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
-            hipLaunchKernelGGL(k_sw_dag_pk, dim3(L.grid), dim3(128), plds, m.stream, c, *(const DagView *)L.view);
+            hipLaunchKernelGGL(k_sw_dag_pk, dim3(L.grid), dim3(192), plds, m.stream, c, *(const DagView *)L.view);
         } else if (wg) {
             const size_t blds = sw_band_lds_bytes(th / bh) + (4 + 2 * (size_t)th) * 4;  // + kept right columns
             if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_wg,
