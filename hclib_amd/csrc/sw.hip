@@ -1333,6 +1333,9 @@ struct SwPkTile {
 // uint4 {sc0(2p), sc1(2p), sc0(2p+1), sc1(2p+1)}. misc[5] = chunks written,
 // misc[6] = chunks read (both reset between tiles).
 constexpr int kSwPkSlots = 2;
+#ifndef HX_SW_PK_PF
+#define HX_SW_PK_PF 3  // sweep operand prefetch distance (groups of 4 steps)
+#endif
 // Timing experiments (diagnostic builds only, results wrong by design):
 // 1 = the score wave computes chunk 0 only and then just publishes the rest,
 // 2 = the sweep wave reads no ring (constant scores)
@@ -1519,22 +1522,27 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
         if (k == 0) tstamp(12);  // the first chunk's scores are there
         const uint4 *src = ring + (size_t)((k % kSwPkSlots) * 32) * 64 + lane;
         uint32_t acc = 0;
-        int4 tn = *(const int4 *)(top + s0);
-        uint4 rn0 = src[0], rn1 = src[64];
+        // operands of group g + kPf are loaded while group g computes
+        constexpr int kPf = HX_SW_PK_PF;
+        int4 tq[kPf + 1];
+        uint4 rq0[kPf + 1], rq1[kPf + 1];
+        auto load_group = [&](int g) {
+            tq[g % (kPf + 1)] = *(const int4 *)(top + s0 + 4 * g);
+            if (HX_SW_PK_EXP == 2) {
+                rq0[g % (kPf + 1)] = make_uint4(g, 2 * g, g, 2 * g);
+                rq1[g % (kPf + 1)] = make_uint4(3 * g, g, 3 * g, g);
+            } else {
+                rq0[g % (kPf + 1)] = src[(2 * g) * 64];
+                rq1[g % (kPf + 1)] = src[(2 * g + 1) * 64];
+            }
+        };
+#pragma unroll
+        for (int g = 0; g < kPf; ++g) load_group(g);
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-            const int4 tc = tn;
-            const uint4 r0 = rn0, r1 = rn1;
-            if (g < 15) {
-                tn = *(const int4 *)(top + s0 + 4 * g + 4);
-                if (HX_SW_PK_EXP == 2) {
-                    rn0 = make_uint4(g, 2 * g, g, 2 * g);
-                    rn1 = make_uint4(3 * g, g, 3 * g, g);
-                } else {
-                    rn0 = src[(2 * g + 2) * 64];
-                    rn1 = src[(2 * g + 3) * 64];
-                }
-            }
+            if (g + kPf < 16) load_group(g + kPf);
+            const int4 tc = tq[g % (kPf + 1)];
+            const uint4 r0 = rq0[g % (kPf + 1)], r1 = rq1[g % (kPf + 1)];
             const int tv[4] = {tc.x, tc.y, tc.z, tc.w};
             const uint32_t s0v[4] = {r0.x, r0.z, r1.x, r1.z}, s1v[4] = {r0.y, r0.w, r1.y, r1.w};
 #pragma unroll

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${1:-gpurun_out/pk}; mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "packed_half or generic_promise_dag or both_schedules" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
-timeout -k 10 300 python -u scripts/sw_pk_variants.py hclib_amd/lib/libhclib_amd.so hclib_amd/lib/pk1w/libhclib_amd.so > $OUT/variants.log 2>&1 || { tail -5 $OUT/variants.log; exit 1; }
+timeout -k 10 300 python -u scripts/sw_pk_variants.py hclib_amd/lib/libhclib_amd.so $VARIANTS > $OUT/variants.log 2>&1 || { tail -5 $OUT/variants.log; exit 1; }
 cat $OUT/variants.log
 timeout -k 10 120 python -u scripts/sw_dag_trace.py $OUT/trace.bin > $OUT/trace.json 2> $OUT/trace.err || { tail -5 $OUT/trace.err; exit 1; }
 rm -f $OUT/trace.bin
