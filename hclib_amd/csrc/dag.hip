@@ -190,7 +190,12 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
         HX_HIP(hipMemcpyAsync(sat.data(), v.satisfied, sat.size() * 4, hipMemcpyDeviceToHost, m.stream));
     }
     HX_HIP(hipStreamSynchronize(m.stream));
-    for (size_t p = 0; p < sat.size(); ++p) satisfied_out[p] = sat[p] ? 1 : 0;
+    bool twice = false;  // tagged puts count satisfied up (hx_dag.h kTagged): 2 = put twice
+    for (size_t p = 0; p < sat.size(); ++p) {
+        satisfied_out[p] = sat[p] ? 1 : 0;
+        twice = twice || sat[p] > 1;
+    }
+    if (twice && !err) err = kErrDoublePut;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
 #if HX_DAG_TRACE

@@ -57,6 +57,9 @@ struct SwCtx {
     int progressive;  // row schedule: chunked bottom-row hand-off
     const int *left_in;  // [nth*th]
     int *right_out;      // [nth*th]
+    // the packed DAG body's outputs as tagged granules {1 << 32 | H}
+    // (bottom rows in gbot [tiles][tw]; right columns [tiles][th]; corners [tiles])
+    unsigned long long *gright, *gcorner;
     int form;            // multi-wave bands: 100 * rows per lane + 10 * skew + hand-off steps / 16
     int bh;              // multi-wave band height (64 * rows per lane)
     // diagnostic build (HX_STAMPS): the DAG's per-task trace (hx_dag.h
@@ -1303,19 +1306,25 @@ constexpr int kSwPkMaxTw = 512;         // f16 exactness bound (see above)
 __host__ __device__ constexpr int sw_pk_topw(int ncols) { return (ncols + 196 + 3) & ~3; }
 __host__ __device__ constexpr int sw_pk_selw(int ncols) { return (ncols + 268 + 3) & ~3; }
 
+// Inputs and outputs in global memory are tagged granules {1 << 32 | H}:
+// a reader polls the tags, so the producing tile's put need not wait for its
+// stores to drain (SwDagPkKind::kTagged).
+typedef unsigned long long sw_gran;
+__device__ __forceinline__ sw_gran sw_granule(int h) { return (1ull << 32) | (uint32_t)h; }
 struct SwPkTile {
     int R0, C0, ncols;
-    const int *corner_src;  // H(R0, C0) from memory (agent scope), or null:
-    int corner_val;         //   this value (every v is G - G(R0, C0))
-    const int *hin;       // top row H (null: the boundary row, R0 == 0)
-    const int *leftcol;   // H(R0 + 1 + k, C0), k < 256, in global memory, or null:
-    const int *left_lds;  //   in LDS (the workgroup ran the left tile), or null: C0 == 0
-    int *hout;            // bottom row H out
-    int *rightcol;        // right column H out (global), may be null
-    int *rightcol_lds;    // ... and in LDS, may be null
-    int *corner_out;      // H(R0 + 256, C0 + ncols) out, may be null
-    int *corner_out_lds;  // ... and in LDS, may be null
-    int *corner_lds;      // H(R0, C0 + ncols) (the top row's last) into LDS, may be null
+    const sw_gran *corner_src;  // H(R0, C0) from memory, or null:
+    int corner_val;             //   this value (every v is G - G(R0, C0))
+    const sw_gran *hin;         // top row (null: the boundary row, R0 == 0, or:)
+    const int *top_lds;         // the top row's H already in LDS, or null
+    const sw_gran *leftcol;     // H(R0 + 1 + k, C0), k < 256, in global memory, or null:
+    const int *left_lds;        //   in LDS (the workgroup ran the left tile), or null: C0 == 0
+    sw_gran *hout;              // bottom row out
+    sw_gran *rightcol;          // right column out (global), may be null
+    int *rightcol_lds;          // ... and in LDS, may be null
+    sw_gran *corner_out;        // H(R0 + 256, C0 + ncols) out, may be null
+    int *corner_out_lds;        // ... and in LDS, may be null
+    int *corner_lds;            // H(R0, C0 + ncols) (the top row's last) into LDS, may be null
     // diagnostic (HX_DAG_TRACE builds): the task's trace record — [8] inputs
     // staged, [10] sweep done, [11] outputs issued; null otherwise
     unsigned long long *trec = nullptr;
@@ -1343,9 +1352,10 @@ constexpr int kSwPkSlots = 2;
 #define HX_SW_PK_EXP 0
 #endif
 constexpr int kSwPkRingU4 = kSwPkSlots * 32 * 64;  // uint4 entries
-// LDS: ring | top | sel x 4 | right columns [2][256] | misc[8] | score rows [4][64]
+// LDS: ring | top | sel x 4 | right columns [2][256] | misc[16] | score rows [4][64] | next top row [512]
+constexpr int kSwPkMisc = 16;
 __host__ __device__ constexpr int sw_pk_lds_words(int tw) {
-    return kSwPkRingU4 * 4 + sw_pk_topw(tw) + 4 * sw_pk_selw(tw) + 2 * kSwPkTh + 8 + 256;
+    return kSwPkRingU4 * 4 + sw_pk_topw(tw) + 4 * sw_pk_selw(tw) + 2 * kSwPkTh + kSwPkMisc + 256 + kSwPkMaxTw;
 }
 inline size_t sw_pk_lds_bytes(int tw) { return (size_t)sw_pk_lds_words(tw) * 4; }
 
@@ -1370,8 +1380,10 @@ __device__ __forceinline__ bool sw_pk_wait(const SwCtx &c, const int *flag, int 
 // (sel) and this lane's four score rows (tbl[q * 64 + lane]). Run for the
 // tile itself, or ahead of time for the right neighbour (the tile the
 // workgroup keeps when its own put releases it) while the sweep still runs.
-template <int KX>
-__device__ void sw_pk_stage(const SwCtx &c, int R0, int C0, int ncols, int *sel, int *tbl) {
+// `mid` runs once the columns the first chunk reads (x < 64) and the score
+// rows are staged (the first chunk's scores can start before the rest).
+template <int KX, class Mid>
+__device__ bool sw_pk_stage(const SwCtx &c, int R0, int C0, int ncols, int *sel, int *tbl, Mid &&mid) {
     const int lane = lane_id();
     const int selw = sw_pk_selw(ncols), xmax = ncols - 1;
     int code[KX];
@@ -1396,8 +1408,7 @@ __device__ void sw_pk_stage(const SwCtx &c, int R0, int C0, int ncols, int *sel,
         return kSwPkNull | ((uint32_t)lo << 8) | (kSwPkNull << 16) | (hs << 24);
     };
     // x = lane + 64 k - 64 for k = 0 .. KX + 5: lo code = code[k - 1], hi = code[k - 2]
-#pragma unroll
-    for (int k = 0; k < KX + 6; ++k) {
+    auto stage = [&](int k) {
         const int x = lane + 64 * k - 64;
         if (x < ncols + 200) {
             const int lo = (k >= 1 && k - 1 < KX) ? code[k - 1] : (int)kSwPkNull;
@@ -1406,22 +1417,29 @@ __device__ void sw_pk_stage(const SwCtx &c, int R0, int C0, int ncols, int *sel,
 #pragma unroll
             for (int o = 0; o < 4; ++o) sel[o * selw + x + 64 + o] = (int)w;
         }
-    }
+    };
+    stage(0);
+    stage(1);
     tbl[lane] = (int)sw_pk_row(s2a);
     tbl[64 + lane] = (int)sw_pk_row(s2b);
     tbl[128 + lane] = (int)sw_pk_row(s2c);
     tbl[192 + lane] = (int)sw_pk_row(s2d);
+    if (!mid()) return false;
+#pragma unroll
+    for (int k = 2; k < KX + 6; ++k) stage(k);
+    return true;
 }
 
 // The score wave: every chunk's scores from the staged selectors and rows.
-__device__ bool sw_pk_scores(const SwCtx &c, int ncols, uint4 *ring, const int *sel, const int *tbl, int *misc) {
+__device__ bool sw_pk_scores(const SwCtx &c, int ncols, uint4 *ring, const int *sel, const int *tbl, int *misc,
+                             int k0 = 0, int k1 = 1 << 30) {
     const int lane = lane_id();
     const int selw = sw_pk_selw(ncols);
     const uint32_t mlo0 = (uint32_t)tbl[lane], mlo1 = (uint32_t)tbl[64 + lane];
     const uint32_t mhi0 = (uint32_t)tbl[128 + lane], mhi1 = (uint32_t)tbl[192 + lane];
     const int *selp = sel + (lane & 3) * selw + 64 + (lane & 3) - lane;  // + s: column s - lane, aligned
     const int nch = (ncols + 127 + 63) / 64;
-    for (int k = 0; k < nch; ++k) {
+    for (int k = k0; k < nch && k < k1; ++k) {
         if (k >= kSwPkSlots && !sw_pk_wait(c, &misc[6], k + 1 - kSwPkSlots)) return false;
         uint4 *dst = ring + (size_t)((k % kSwPkSlots) * 32) * 64 + lane;
         const int *sp = selp + 64 * k;
@@ -1452,31 +1470,55 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
     const int topw = sw_pk_topw(ncols);
     // --- loads, all issued before any is used, none predicated (a
     // predicated load becomes a branch that waits for it on its own): the left
-    // column, the top row and the corner (other tasks' outputs). Unused
-    // operands read a valid word and are discarded.
+    // column, the top row and the corner (other tasks' granules, polled until
+    // every tag is set — normally at once: their stores were issued before the
+    // puts that released this tile). Unused operands read a valid word.
     const int xmax = ncols - 1;
     int rowq[4];  // matrix rows of lo q0, lo q1, hi q0, hi q1
     rowq[0] = R0 + 1 + 2 * lane;
     rowq[1] = rowq[0] + 1;
     rowq[2] = rowq[0] + 128;
     rowq[3] = rowq[1] + 128;
-    int lg[4];
     const bool lglob = T.leftcol != nullptr;
-    const int *lsrc = lglob ? T.leftcol : T.hout;
+    const sw_gran *lsrc = lglob ? T.leftcol : T.hout;
+    const sw_gran *hsrc = T.hin ? T.hin : T.hout;
+    sw_gran lg[4], th_[KX], cg = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) lg[q] = ld_agent(&lsrc[lglob ? rowq[q] - R0 - 1 : 0]);
-    int th_[KX];
-    const int *hsrc = T.hin ? T.hin : T.hout;
+    for (int q = 0; q < 4; ++q) lg[q] = 0;
 #pragma unroll
-    for (int k = 0; k < KX; ++k) {
-        const int x = lane + 64 * k;
-        th_[k] = ld_agent(&hsrc[T.hin ? (x < ncols ? x : xmax) : 0]);
+    for (int k = 0; k < KX; ++k) th_[k] = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    // (a kept tile whose top row the score wave already took reads nothing)
+    for (uint32_t n = 0; T.hin || lglob || T.corner_src; ++n) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lg[q] = ld_agent(&lsrc[lglob ? rowq[q] - R0 - 1 : 0]);
+#pragma unroll
+        for (int k = 0; k < KX; ++k) {
+            const int x = lane + 64 * k;
+            th_[k] = ld_agent(&hsrc[T.hin ? (x < ncols ? x : xmax) : 0]);
+        }
+        cg = ld_agent(T.corner_src ? T.corner_src : T.hout);
+        bool ready = !T.corner_src || (cg >> 32) == 1ull;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ready = ready && (!lglob || (lg[q] >> 32) == 1ull);
+#pragma unroll
+        for (int k = 0; k < KX; ++k) ready = ready && (!T.hin || (th_[k] >> 32) == 1ull);
+        if (__ballot(!ready) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
+        if ((n & 63) == 63) {
+            if (ld_agent(c.err)) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
+                if (lane == 0) dev_error(c.err, kErrSpinTimeout);
+                return false;
+            }
+        }
     }
-    const int cget = ld_agent(T.corner_src ? T.corner_src : T.hout);
+    const int cget = (int)(uint32_t)cg;
     int lh[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        lh[q] = T.left_lds ? *((const lds_i32 *)T.left_lds + (rowq[q] - R0 - 1)) : (lglob ? lg[q] : -rowq[q]);
+        lh[q] = T.left_lds ? *((const lds_i32 *)T.left_lds + (rowq[q] - R0 - 1))
+                           : (lglob ? (int)(uint32_t)lg[q] : -rowq[q]);
     // --- the left column as packed v
     const int base = (T.corner_src ? cget : T.corner_val) + R0 + C0;  // G(R0, C0)
     uint32_t l16[4];
@@ -1489,7 +1531,9 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
         const int x = lane + 64 * k;
         if (x < topw) {
             int v = 0;
-            if (k < KX && x < ncols) v = T.hin ? th_[k] + R0 + (C0 + 1 + x) - base : -base;
+            if (k < KX && x < ncols)
+                v = T.hin ? (int)(uint32_t)th_[k] + R0 + (C0 + 1 + x) - base
+                          : (T.top_lds ? *((const lds_i32 *)T.top_lds + x) + R0 + (C0 + 1 + x) - base : -base);
             top[x] = (int)sw_f16_bits(v);
         }
     }
@@ -1500,7 +1544,8 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
             int h = -(C0 + ncols);
 #pragma unroll
             for (int k = 0; k < KX; ++k)
-                if (k == (xl >> 6) && T.hin) h = th_[k];
+                if (k == (xl >> 6) && T.hin) h = (int)(uint32_t)th_[k];
+            if (T.top_lds) h = *((const lds_i32 *)T.top_lds + xl);
             *T.corner_lds = h;
         }
     }
@@ -1571,9 +1616,9 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
             if (lane >= 32 && x >= 0 && x < ncols) {
                 const sw_h2 pv = sw_as_h2(acc);
                 const int h = (int)(float)(e ? pv.y : pv.x) + base - Rb - (C0 + 1 + x);
-                st_agent(&T.hout[x], h);
+                st_agent(&T.hout[x], sw_granule(h));
                 if (x == ncols - 1) {
-                    if (T.corner_out) st_agent(T.corner_out, h);
+                    if (T.corner_out) st_agent(T.corner_out, sw_granule(h));
                     if (T.corner_out_lds) *T.corner_out_lds = h;
                 }
             }
@@ -1590,7 +1635,7 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int k = rowq[q] - R0 - 1;
-        if (T.rightcol) st_agent(&T.rightcol[k], rv[q]);
+        if (T.rightcol) st_agent(&T.rightcol[k], sw_granule(rv[q]));
         if (T.rightcol_lds) T.rightcol_lds[k] = rv[q];
     }
     tstamp(11);
@@ -1605,14 +1650,17 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
 struct SwDagPkKind {
     using Ctx = SwCtx;
     static constexpr bool kSc1Payload = true;  // tile inputs/outputs move by ld_agent / st_agent
+    static constexpr bool kTagged = true;      // ... as tagged granules: puts without a drain
     __device__ static int *misc_of(const SwCtx &c) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
-        return sw_lds + sw_pk_lds_words(c.tw) - 8 - 256;
+        return sw_lds + sw_pk_lds_words(c.tw) - kSwPkMisc - 256 - kSwPkMaxTw;
     }
     // misc: [0] the workgroup's last tile, [1..2] kept corners by parity,
     // [3] the corner datum, [4] the finished tile + 1 (wave 1 waits on it),
     // [5] / [6] score chunks written / read, [7] the tile whose selectors and
-    // score rows are staged (misc + 8: the rows, [4][64])
+    // score rows are staged (misc + 16: the rows, [4][64]), [8] the tile whose
+    // top row (H) is in LDS (misc + 16 + 256: the right neighbour's top row,
+    // taken while this tile runs once every granule's tag is set)
     __device__ static bool run_group(const SwCtx &c, uint32_t t, const uint32_t *, int wave) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
         int *misc = misc_of(c);
@@ -1625,20 +1673,60 @@ struct SwDagPkKind {
             return sw_pk_wait(c, &misc[4], (int)t + 1);
         }
         if (wave == 1) {
-            int *tbl = misc + 8;
-            // staged ahead (misc[7] == t) or now
+            int *tbl = misc + kSwPkMisc;
+            // staged ahead (misc[7] == t), or now: the first chunk's scores as
+            // soon as its columns are staged, the rest after
+            bool ok = true;
             if (misc[7] != (int)t) {
-                if (c.tw <= 256) sw_pk_stage<4>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl);
-                else sw_pk_stage<8>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl);
+                auto first = [&]() { return sw_pk_scores(c, c.tw, ring, sel, tbl, misc, 0, 1); };
+                ok = c.tw <= 256 ? sw_pk_stage<4>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl, first)
+                                 : sw_pk_stage<8>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl, first);
+                if (ok) ok = sw_pk_scores(c, c.tw, ring, sel, tbl, misc, 1);
+            } else {
+                ok = sw_pk_scores(c, c.tw, ring, sel, tbl, misc);
             }
-            if (!sw_pk_scores(c, c.tw, ring, sel, tbl, misc)) return false;
+            if (!ok) return false;
             // while the sweep runs: stage the right neighbour
             const bool next = j + 1 < c.ntw;
+            auto none = []() { return true; };
             if (next) {
-                if (c.tw <= 256) sw_pk_stage<4>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl);
-                else sw_pk_stage<8>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl);
+                if (c.tw <= 256) sw_pk_stage<4>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl, none);
+                else sw_pk_stage<8>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl, none);
             }
             if (lane_id() == 0) misc[7] = next ? (int)t + 1 : -1;
+            // ... and its top row (the up-right tile's bottom row), polled
+            // while this tile's sweep runs: kept, the right neighbour then
+            // starts without a global load
+            // (after the sweep wave has read this tile's own LDS top row: it
+            // consumes chunk 0 only after that)
+            if (next && i > 0 && sw_pk_wait(c, &misc[6], 1)) {
+                int *ntop = misc + kSwPkMisc + 256;
+                const sw_gran *src = c.gbot + (size_t)(t + 1 - (uint32_t)c.ntw) * c.tw;
+                const int xmax = c.tw - 1;
+                for (uint32_t n = 0;; ++n) {
+                    sw_gran g[kSwPkMaxTw / 64];
+                    bool ready = true;
+#pragma unroll
+                    for (int k = 0; k < kSwPkMaxTw / 64; ++k) {
+                        const int x = lane_id() + 64 * k;
+                        g[k] = k * 64 < c.tw ? ld_agent(&src[x < c.tw ? x : xmax]) : (1ull << 32);
+                    }
+#pragma unroll
+                    for (int k = 0; k < kSwPkMaxTw / 64; ++k) ready = ready && (g[k] >> 32) == 1ull;
+                    if (__ballot(!ready) == 0) {
+#pragma unroll
+                        for (int k = 0; k < kSwPkMaxTw / 64; ++k) {
+                            const int x = lane_id() + 64 * k;
+                            if (x < c.tw) ntop[x] = (int)(uint32_t)g[k];
+                        }
+                        if (lane_id() == 0) lds_flag_st(&misc[8], (int)t + 1);
+                        break;
+                    }
+                    // give up once this tile's sweep is done (the next one loads it)
+                    if (lds_flag_ld(&misc[4]) == (int)t + 1) break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+            }
             return true;
         }
         const bool from_lds = j > 0 && misc[0] == (int)t - 1;
@@ -1646,15 +1734,17 @@ struct SwDagPkKind {
         T.R0 = i * kSwPkTh;
         T.C0 = j * c.tw;
         T.ncols = c.tw;
-        T.corner_src = (T.R0 == 0 || j == 0 || from_lds) ? nullptr : &c.corner[t - (uint32_t)c.ntw - 1];
+        T.corner_src = (T.R0 == 0 || j == 0 || from_lds) ? nullptr : &c.gcorner[t - (uint32_t)c.ntw - 1];
         T.corner_val = T.R0 == 0 ? -T.C0 : (j == 0 ? -T.R0 : (from_lds ? misc[1 + ((t - 1) & 1)] : 0));
-        T.hin = i > 0 ? c.bottom + (size_t)(t - (uint32_t)c.ntw) * c.tw : nullptr;
+        T.hin = i > 0 ? c.gbot + (size_t)(t - (uint32_t)c.ntw) * c.tw : nullptr;
+        T.top_lds = (i > 0 && from_lds && misc[8] == (int)t) ? misc + kSwPkMisc + 256 : nullptr;
+        if (T.top_lds) T.hin = nullptr;
         T.left_lds = j > 0 && from_lds ? right_keep + ((t - 1) & 1) * kSwPkTh : nullptr;
-        T.leftcol = j > 0 && !from_lds ? c.right + (size_t)(t - 1) * kSwPkTh : nullptr;
-        T.hout = c.bottom + (size_t)t * c.tw;
-        T.rightcol = c.right + (size_t)t * kSwPkTh;
+        T.leftcol = j > 0 && !from_lds ? c.gright + (size_t)(t - 1) * kSwPkTh : nullptr;
+        T.hout = c.gbot + (size_t)t * c.tw;
+        T.rightcol = c.gright + (size_t)t * kSwPkTh;
         T.rightcol_lds = right_keep + (t & 1) * kSwPkTh;
-        T.corner_out = c.corner + t;
+        T.corner_out = c.gcorner + t;
         T.corner_out_lds = &misc[3];
         T.corner_lds = &misc[1 + (t & 1)];
         T.trec = HX_DAG_TRACE && c.dtrace ? c.dtrace + (size_t)t * kDagTraceWords : nullptr;
@@ -1693,6 +1783,7 @@ __global__ __launch_bounds__(192) void k_sw_dag_pk(SwCtx c, DagView v) {
         misc[5] = 0;
         misc[6] = 0;
         misc[7] = -1;  // no tile's scores staged
+        misc[8] = -1;  // no tile's top row in LDS
     }
     run_dag_group<SwDagPkKind>(c, v, nullptr);
 }
@@ -1748,13 +1839,17 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     const int form = sw_pick_form(th, dag ? 214 : 412), bh = sw_form_bh(form);
     const bool band_shape = sw_band_ok(th, bh) && tw <= 65536;
     const bool band = rows && band_shape && !(sched && !strcmp(sched, "rows1"));
+    // the promise DAG's 256-row tiles at most 512 wide: the packed-half body,
+    // tagged outputs (HCLIB_HIP_SW_PK=0: the band forms)
+    const bool pk = dag && th == kSwPkTh && tw <= kSwPkMaxTw && env_int("HCLIB_HIP_SW_PK", 1) != 0;
     const size_t nt = ntw * nth;
     const size_t b_s1 = ntw * tw, b_s2 = nth * th;
-    const size_t b_bot = rows ? 0 : nt * tw * 4, b_right = rows ? 0 : nt * th * 4, b_c = nt * 4,
-                 b_dep = nt * 4, b_ready = nt * 4, b_gbot = rows ? nt * tw * 8 : 0;
+    const size_t b_bot = (rows || pk) ? 0 : nt * tw * 4, b_right = (rows || pk) ? 0 : nt * th * 4, b_c = nt * 4,
+                 b_dep = nt * 4, b_ready = nt * 4, b_gbot = (rows || pk) ? nt * tw * 8 : 0,
+                 b_gright = pk ? nt * th * 8 : 0, b_gc = pk ? nt * 8 : 0;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t total = al(b_s1) + al(b_s2) + al(b_bot) + al(b_right) + al(b_c) + al(b_dep) +
-                         al(b_ready) + al(b_gbot) + 1024;
+                         al(b_ready) + al(b_gbot) + al(b_gright) + al(b_gc) + 1024;
     char *d = nullptr;
     if (hipMalloc((void **)&d, total) != hipSuccess) {
         set_error("hclib_hip_sw: hipMalloc(%zu) failed", total);
@@ -1770,6 +1865,8 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     c.deps = (uint32_t *)(d + off); off += al(b_dep);
     c.ready = (uint32_t *)(d + off); off += al(b_ready);
     c.gbot = (unsigned long long *)(d + off); off += al(b_gbot);
+    c.gright = (unsigned long long *)(d + off); off += al(b_gright);
+    c.gcorner = (unsigned long long *)(d + off); off += al(b_gc);
     uint32_t *misc = (uint32_t *)(d + off);
     c.ready_tail = misc;
     c.ready_head = misc + 64;
@@ -1799,10 +1896,14 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         uint32_t one = 1;  // tile 0 already sits at ready[0]
         if ((rc = hip_check(hipMemcpyAsync(c.ready_tail, &one, 4, hipMemcpyHostToDevice, m.stream), "tail"))) return fail(rc);
     }
-    if (rows) {
+    if (rows || pk) {
         // every granule's tag starts at 0 (not yet put)
         if ((rc = hip_check(hipMemsetAsync(c.gbot, 0, b_gbot, m.stream), "memset granules"))) return fail(rc);
-    } else {
+        if (pk && (rc = hip_check(hipMemsetAsync(c.gright, 0, al(b_gright) + b_gc, m.stream),
+                                  "memset granules")))
+            return fail(rc);
+    }
+    if (!rows) {
         hipLaunchKernelGGL(k_sw_init, dim3(1024), dim3(256), 0, m.stream, c.deps, c.ready, c.ntw, c.nth);
     }
     const size_t lds = band ? sw_band_lds_bytes(th / bh)
@@ -1837,9 +1938,6 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         // tile tasks on workgroups of th / 64 + 2 waves where the band
         // kernel applies (HCLIB_HIP_SW_DAG_WAVE=1: one wave per tile)
         const bool wg = band_shape && env_int("HCLIB_HIP_SW_DAG_WAVE", 0) == 0;
-        // 256-row tiles at most 512 wide: the packed-half body, one wave per
-        // tile (HCLIB_HIP_SW_PK=0: the band forms above)
-        const bool pk = th == kSwPkTh && tw <= kSwPkMaxTw && env_int("HCLIB_HIP_SW_PK", 1) != 0;
         hclib_hip_dag_launch_t L;
         if ((rc = hclib_hip_dag_begin((uint32_t)nt, (uint32_t)(3 * nt), 0, nullptr, off.data(), ids.data(), nullptr,
                                       nullptr, pk ? env_int("HCLIB_HIP_SW_PK_WGS_PER_CU", 1)
@@ -1862,7 +1960,9 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         } else {
             hipLaunchKernelGGL(k_sw_dag, dim3(L.grid), dim3(64), lds, m.stream, c, *(const DagView *)L.view);
         }
-        if ((rc = hclib_hip_dag_end("hclib_hip_sw (dag)", nullptr, nullptr, &dst))) return fail(rc);
+        // (the packed body's tagged puts are checked for double puts here)
+        std::vector<uint8_t> sat(pk ? 3 * nt : 0);
+        if ((rc = hclib_hip_dag_end("hclib_hip_sw (dag)", nullptr, pk ? sat.data() : nullptr, &dst))) return fail(rc);
     } else {
         if ((rc = hip_check(hipEventRecord(m.ev0, m.stream), "event"))) return fail(rc);
         if (band) {
@@ -1907,6 +2007,10 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         // the edges the row schedule resolved: each tile's up, left and
         // diagonal futures (the same 3-per-interior-tile count as the queue)
         st[1] = 3ull * (ntw - 1) * (nth - 1) + (ntw - 1) + (nth - 1);
+    } else if (pk) {
+        unsigned long long g = 0;  // the last tile's corner granule
+        (void)hipMemcpy(&g, c.gcorner + (nt - 1), 8, hipMemcpyDeviceToHost);
+        corner = (int)(uint32_t)g;
     } else {
         (void)hipMemcpy(&corner, c.corner + (nt - 1), 4, hipMemcpyDeviceToHost);
     }

@@ -330,6 +330,19 @@ struct group_put_n { static constexpr int value = 0; };
 template <class K>
 struct group_put_n<K, decltype((void)K::kPutN)> { static constexpr int value = K::kPutN; };
 
+// Optional: static constexpr bool kTagged = true — the Kind's bodies publish
+// their outputs as tagged words and their readers poll the tags, so a put
+// need not wait for the outputs' stores to drain before it releases the
+// waiters (run_dag_group skips that drain). Such a put counts `satisfied` up
+// instead of exchanging it (no result to wait for): a double put leaves 2,
+// which hclib_hip_dag_end reports after the launch. Its datums are published
+// without a drain too: they are for the host (read after the launch), not
+// for device readers of the promise.
+template <class K, class = void>
+struct group_tagged { static constexpr bool value = false; };
+template <class K>
+struct group_tagged<K, decltype((void)K::kTagged)> { static constexpr bool value = K::kTagged; };
+
 // Optional: static void after_body(const Ctx&, uint32_t task), run by every
 // thread once every wave has finished the task's body (before its put).
 template <class K, class = void>
@@ -348,6 +361,7 @@ struct DagGroupShared {
     uint32_t npend;       // tasks the last put released for the ready list
     uint32_t skip;        // 1: the last put kept a task (its ready slot is a skip)
     uint32_t dbl;         // the running task put a promise twice
+    uint32_t fail;        // a wave's body failed (device error): every wave leaves
     uint32_t waiter[64];  // their ids, concatenated in promise order
     uint32_t pend[64];
 };
@@ -369,6 +383,8 @@ template <class Kind>
 __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view, uint32_t *slot_unused) {
     (void)slot_unused;
     constexpr int N = group_put_n<Kind>::value;
+    constexpr bool kTagged = group_tagged<Kind>::value;
+    static_assert(!kTagged || (N > 0 && Kind::kSc1Payload), "tagged puts use the split put of sc1 payloads");
     __shared__ DagGroupShared sh;
     DagWave w{view, 0, 0, kDagEmpty, 0, 0};
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6), nwaves = (int)(blockDim.x >> 6);
@@ -389,6 +405,7 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
     if (threadIdx.x == 0) {
         sh.npend = 0;
         sh.skip = 0;
+        sh.fail = 0;
     }
     __syncthreads();
     stamp(0);
@@ -513,22 +530,35 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
                     }
                 if (lane < N) {
                     st_agent(&view.datum[my_p], my_d);
-                    was = __hip_atomic_exchange(&view.satisfied[my_p], 1u, __ATOMIC_RELAXED, HX_AGENT);
+                    if constexpr (kTagged)  // no result to wait for: a second put leaves 2 (hclib_hip_dag_end)
+                        __hip_atomic_fetch_add(&view.satisfied[my_p], 1u, __ATOMIC_RELAXED, HX_AGENT);
+                    else
+                        was = __hip_atomic_exchange(&view.satisfied[my_p], 1u, __ATOMIC_RELAXED, HX_AGENT);
                 }
             }
         }
         // every wave's outputs are visible before wave 0 releases the waiters:
         // sc1 payloads need only the drain, plain stores the agent release
         // (another XCD's L2 must not serve stale lines)
-        if constexpr (Kind::kSc1Payload) vm_drain();
-        else release_agent();
-        if constexpr (N > 0) {
-            if (wave == helper) {
-                const bool dbl = __ballot(lane < N && was != 0) != 0;  // src/hclib-promise.c:206-207
-                if (lane == 0) sh.dbl = dbl ? 1u : 0u;
+        if constexpr (kTagged) {
+            // no drain: the readers poll the outputs' tags; a double put is
+            // found after the launch (a satisfied count of 2)
+            if (wave == helper && lane == 0) sh.dbl = 0u;
+        } else {
+            if constexpr (Kind::kSc1Payload) vm_drain();
+            else release_agent();
+            if constexpr (N > 0) {
+                if (wave == helper) {
+                    const bool dbl = __ballot(lane < N && was != 0) != 0;  // src/hclib-promise.c:206-207
+                    if (lane == 0) sh.dbl = dbl ? 1u : 0u;
+                }
             }
         }
-        if (__syncthreads_or(!ok)) break;
+        // (an LDS flag and a plain barrier: __syncthreads_or reads the
+        // workgroup size from memory and so waits for every store in flight)
+        if (!ok) sh.fail = 1u;
+        __syncthreads();
+        if (sh.fail) break;
         // every wave is done with the task: the Kind's between-task work
         // (e.g. resetting its LDS hand-off flags so the next body needs no
         // barrier of its own)

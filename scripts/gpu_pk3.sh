@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${1:-gpurun_out/pk}; mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "packed_half or generic_promise_dag or both_schedules" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "packed_half or generic_promise_dag or both_schedules or dag or sw" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
 timeout -k 10 300 python -u scripts/sw_pk_variants.py hclib_amd/lib/libhclib_amd.so $VARIANTS > $OUT/variants.log 2>&1 || { tail -5 $OUT/variants.log; exit 1; }
 cat $OUT/variants.log
