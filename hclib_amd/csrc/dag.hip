@@ -83,6 +83,10 @@ extern "C" int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t
     uint32_t nready = 0;
     for (uint32_t t = 0; t < ntasks; ++t)
         if (deps[t] == 0) ready[nready++] = t;
+    // a group Kind with reserved puts (hx_dag.h kReserve) gives every waiter
+    // entry a ready slot of its own: nready + the registered awaits in all
+    const uint32_t nslots = nready + woff[npromises];
+    if (nslots > ready.size()) ready.resize(nslots, kDagEmpty);
     std::vector<unsigned long long> datum(npromises ? npromises : 1, 0);
     std::vector<uint32_t> sat(npromises ? npromises : 1, 0);
     for (uint32_t p = 0; preput && p < npromises; ++p)
@@ -101,7 +105,7 @@ extern "C" int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t
     const size_t o_sat = o_datum + up256(datum.size() * 8);
     const size_t o_pay = o_sat + up256(sat.size() * 4);
     const size_t o_ready = o_pay + up256((size_t)ntasks * payload_words * 4 + 4);
-    const size_t bytes = o_ready + up256((size_t)ntasks * 4 + 4);
+    const size_t bytes = o_ready + up256(ready.size() * 4 + 4);
     std::vector<char> h(bytes, 0);
     uint32_t *ctl = (uint32_t *)&h[o_ctl];
     ctl[64] = nready;  // tail
@@ -137,6 +141,7 @@ extern "C" int hclib_hip_dag_begin(uint32_t ntasks, uint32_t npromises, uint32_t
     v.payload = (const uint32_t *)(d + o_pay);
     v.ready = (uint32_t *)(d + o_ready);
     v.ntasks = ntasks;
+    v.nslots = nslots;
     v.npromises = npromises;
     v.payload_words = payload_words;
     v.trace = nullptr;

@@ -1651,6 +1651,7 @@ struct SwDagPkKind {
     using Ctx = SwCtx;
     static constexpr bool kSc1Payload = true;  // tile inputs/outputs move by ld_agent / st_agent
     static constexpr bool kTagged = true;      // ... as tagged granules: puts without a drain
+    static constexpr bool kReserve = true;     // ready slots taken beside the counter decrements
     __device__ static int *misc_of(const SwCtx &c) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
         return sw_lds + sw_pk_lds_words(c.tw) - kSwPkMisc - 256 - kSwPkMaxTw;

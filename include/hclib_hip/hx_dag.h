@@ -52,6 +52,7 @@ struct DagView {
     uint32_t *err;               // DevError
     unsigned long long *stats;   // [0] tasks run, [1] puts, [2] releases
     uint32_t ntasks, npromises, payload_words, spin_ms;
+    uint32_t nslots;             // ready slots with reserved puts: initially ready + every waiter entry
     // diagnostic builds (HX_STAMPS, HX_TRACE) with HCLIB_HIP_DAG_TRACE set: per task
     // kDagTraceWords 100 MHz stamps (see run_dag_group); null otherwise
     unsigned long long *trace;
@@ -343,6 +344,18 @@ struct group_tagged { static constexpr bool value = false; };
 template <class K>
 struct group_tagged<K, decltype((void)K::kTagged)> { static constexpr bool value = K::kTagged; };
 
+// Optional: static constexpr bool kReserve = true — every put takes one ready
+// slot per waiter entry of its promises with one tail fetch-add issued beside
+// its counter decrements, and fills them at once: a released task's id, or
+// kDagSkip (kept, or not released). The put's other releases then reach the
+// ready list one round trip sooner than through the helper's append at the
+// next task; the list holds view.nslots entries (hclib_hip_dag_begin), and
+// tickets run to that count. Needs at most 64 waiter entries per task.
+template <class K, class = void>
+struct group_reserve { static constexpr bool value = false; };
+template <class K>
+struct group_reserve<K, decltype((void)K::kReserve)> { static constexpr bool value = K::kReserve; };
+
 // Optional: static void after_body(const Ctx&, uint32_t task), run by every
 // thread once every wave has finished the task's body (before its put).
 template <class K, class = void>
@@ -384,6 +397,9 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
     (void)slot_unused;
     constexpr int N = group_put_n<Kind>::value;
     constexpr bool kTagged = group_tagged<Kind>::value;
+    constexpr bool kReserve = group_reserve<Kind>::value;
+    static_assert(!kReserve || N > 0, "reserved puts use the split put");
+    const uint32_t nslots = kReserve ? view.nslots : view.ntasks;
     static_assert(!kTagged || (N > 0 && Kind::kSc1Payload), "tagged puts use the split put of sc1 payloads");
     __shared__ DagGroupShared sh;
     DagWave w{view, 0, 0, kDagEmpty, 0, 0};
@@ -428,7 +444,7 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
                 if (lane == 0) ticket = add_agent(view.head, 1u);
                 ticket = (uint32_t)__shfl((int)ticket, 0, 64);
                 t = kDagEmpty;
-                if (ticket >= view.ntasks) break;
+                if (ticket >= nslots) break;
                 if (lane == 0) {
                     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                     while ((t = ld_agent(&view.ready[ticket])) == kDagEmpty) {
@@ -571,6 +587,9 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
             if (wave == 0) {
                 const uint32_t nwait = sh.nwait;
                 if (nwait > 64) {
+                    // (reserved puts need <= 64 waiter entries: the ordinary put
+                    // below appends releases only, so the slot count would be off)
+                    if (kReserve && lane == 0) dev_error(view.err, kErrBadTask);
                     uint32_t p[N];
                     unsigned long long d[N];
                     Kind::promises(ctx, t, p);
@@ -583,6 +602,36 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
                         sh.npend = 0;
                         sh.skip = 0;
                     }
+                } else if (kReserve) {
+                    // one slot per waiter entry, taken beside the decrements
+                    uint32_t base = 0, rt = kDagEmpty, c = 0;
+                    if (lane == 0) base = add_agent(view.tail, nwait);
+                    if ((uint32_t)lane < nwait) {
+                        c = sh.waiter[lane];
+                        if (add_agent(&view.deps[c], (uint32_t)-1) == 1u) rt = c;
+#if HX_DAG_TRACE
+                        if (view.trace && rt == c) {
+                            view.trace[(size_t)c * kDagTraceWords + 0] = __builtin_amdgcn_s_memrealtime();
+                            view.trace[(size_t)c * kDagTraceWords + 6] = t;
+                        }
+#endif
+                    }
+                    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+                    const unsigned long long m = __ballot(rt != kDagEmpty);
+                    int kept_lane = -1;
+                    if (m) {  // keep the first released task (see dag_put_one)
+                        kept_lane = __builtin_ctzll(m);
+                        w.next = (uint32_t)__builtin_amdgcn_readlane((int)rt, kept_lane);
+                    }
+                    if ((uint32_t)lane < nwait)
+                        st_agent(&view.ready[base + (uint32_t)lane], (rt != kDagEmpty && lane != kept_lane) ? rt : kDagSkip);
+                    if (lane == 0) {
+                        sh.npend = 0;
+                        sh.skip = 0;
+                    }
+                    w.puts += N;
+                    w.releases += (unsigned long long)__builtin_popcountll(m);
+                    w.skip_lane = 0;
                 } else {
                     const bool dbl = sh.dbl != 0;
                     if (dbl && lane == 0) dev_error(view.err, kErrDoublePut);
