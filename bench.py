@@ -79,10 +79,16 @@ def wide_tree(H, rank, world, be, steps=2, split=7):
         # region): T(1) for the efficiency T(1) / (N * T(N))
         dist.barrier(world, be)
         t1 = time.perf_counter()
-        H.uts(T1XL)
+        r1 = H.uts(T1XL)
         one = dist.max_over_ranks(time.perf_counter() - t1, world, be)
         out["ms_one_gpu"] = one * 1e3
         out["efficiency"] = one / (world * el / steps)
+        # the same from the GPUs' own clocks: the whole tree's kernel time
+        # over N x the slowest rank's (what wall-clock skew and host overhead
+        # cannot blur; the partition's own balance)
+        k1 = dist.max_over_ranks(r1["kernel_ms"], world, be)
+        out["kernel_ms_one_gpu"] = k1
+        out["projected_efficiency_kernel"] = k1 / (world * max(per_rank))
     return out
 
 
@@ -484,25 +490,38 @@ def main():
         t1 = time.perf_counter()
         H.uts(T3L)
         t3l_one = dist.max_over_ranks(time.perf_counter() - t1, world, be)
-    wide = None if args.no_extras else wide_tree(H, rank, world, be)
+    # N > 1: every optional leg runs under a wall-clock guard (dist.LegGuard):
+    # a leg that stalls (a rank lost in a collective, a kernel that never
+    # returns) is reported as failed in the line, the remaining legs are
+    # skipped on every rank, and the line still prints within the bound
+    legs = dist.LegGuard(world, float(os.environ.get("HCLIB_BENCH_LEG_TIMEOUT_S", "120")),
+                         device=(0 if args.share_device else local) if be == "nccl" or args.share_device else None) \
+        if world > 1 else None
+    guarded = (lambda name, fn: legs.run(name, fn)) if legs else (lambda name, fn: fn())
+    wide = None if args.no_extras else guarded("wide_tree", lambda: wide_tree(H, rank, world, be))
     shard_tri = None
     if world > 1 and not args.no_extras:
         # the 2^28 triad block-sharded over the ranks (no
         # exchange); whole-job GB/s over the slowest rank's launch time
-        n_local = (1 << 28) // world
-        tr = measure_triad(H, n=n_local, sync=lambda: dist.barrier(world, be))
-        ms = dist.max_over_ranks(tr["ms"], world, be)
-        ok = dist.max_over_ranks(0.0 if tr["bit_exact"] else 1.0, world, be) == 0.0
-        shard_tri = {"workload": f"hclib_forasync 1-D triad, 2^28 fp32 block-sharded over {world} GPU(s)",
-                     "GB_per_s": 12 * n_local * world / ms / 1e6, "ms": ms, "scaling": "strong",
-                     "bit_exact": ok}
+        def sharded_triad():
+            n_local = (1 << 28) // world
+            tr = measure_triad(H, n=n_local, sync=lambda: dist.barrier(world, be))
+            ms = dist.max_over_ranks(tr["ms"], world, be)
+            ok = dist.max_over_ranks(0.0 if tr["bit_exact"] else 1.0, world, be) == 0.0
+            return {"workload": f"hclib_forasync 1-D triad, 2^28 fp32 block-sharded over {world} GPU(s)",
+                    "GB_per_s": 12 * n_local * world / ms / 1e6, "ms": ms, "scaling": "strong",
+                    "bit_exact": ok}
+        shard_tri = guarded("forasync_sharded", sharded_triad)
     shard_sw = None
     if world > 1 and not args.no_extras:
-        shard_sw = sharded_sw(H, rank, world, be)
+        shard_sw = guarded("sw_sharded", lambda: sharded_sw(H, rank, world, be))
     skewed = None
     if world > 1 and not args.no_extras and os.environ.get("HCLIB_BENCH_SHARE_WORK", "1") != "0":
-        skewed = skewed_sharing(H, rank, world, be)
+        skewed = guarded("uts_work_sharing", lambda: skewed_sharing(H, rank, world, be))
+    stalled = bool(legs and legs.stalled)
     if rank != 0:
+        if stalled:  # a leg's thread may still sit in a collective: no orderly shutdown
+            os._exit(0)
         dist.shutdown(world)
         return
 
@@ -535,6 +554,8 @@ def main():
     if t3l_one is not None:
         out["ms_one_gpu"] = t3l_one * 1e3
         out["efficiency"] = t3l_one / (world * elapsed / args.steps)
+    if stalled:
+        out["legs_stalled"] = True
     if wide:
         out["wide_tree"] = wide
     if shard_tri:
@@ -621,6 +642,8 @@ def main():
         out["gpu_over_one_cpu_worker"] = value / out["cpu_baseline"]["one_worker_nodes_per_s"]
         out["cpu_configs"] = cpu_configs(allot["threads"], s1, s2, out["configs"])
     print(json.dumps(out), flush=True)
+    if stalled:
+        os._exit(0)
     dist.shutdown(world)
 
 

@@ -133,6 +133,7 @@ def lib():
         L.hclib_hip_ipc_export.argtypes = [C.c_void_p, C.c_void_p]
         L.hclib_hip_ipc_import.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
         L.hclib_hip_ipc_close.argtypes = [C.c_void_p]
+        L.hclib_hip_last_timeline.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
 
@@ -373,3 +374,25 @@ def last_narrow_counters():
     out = (C.c_uint64 * 4)()
     lib().hclib_hip_last_narrow_counters(out)
     return list(out)
+
+
+TIMELINE_EVENTS = {1: "start", 2: "busy", 3: "idle", 4: "spill", 5: "term", 6: "end"}
+
+
+def last_timeline():
+    """Worker timelines of the last megakernel launch (a `--variant timeline`
+    library run with HCLIB_HIP_TIMELINE=<events per worker>, hx_sched.h
+    Timeline): per worker a list of (time in 10 ns ticks, event, value)."""
+    per = C.c_uint32()
+    nw = lib().hclib_hip_last_timeline(None, 0, C.byref(per))
+    if nw <= 0 or per.value == 0:
+        return []
+    import numpy as np
+    buf = np.zeros(nw * per.value, dtype=np.uint64)
+    lib().hclib_hip_last_timeline(buf.ctypes.data, buf.size, C.byref(per))
+    buf = buf.reshape(nw, per.value)
+    out = []
+    for w in range(nw):
+        row = buf[w][buf[w] != 0]
+        out.append([(int(v >> 24), int((v >> 20) & 0xF), int(v & 0xFFFFF)) for v in row])
+    return out

@@ -35,7 +35,7 @@ CFLAGS = [
 ]
 
 
-VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "trace": ["-DHX_TRACE=1"],
+VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "trace": ["-DHX_TRACE=1"], "timeline": ["-DHX_TIMELINE=1"],
             # SW band-sweep timing experiments (wrong results by design: sw.hip HX_SW_EXP)
             "pkexp1": ["-DHX_SW_PK_EXP=1"], "pk1w": ["-DHX_PK1W=1"], "untag": ["-DHX_UNTAG=1"], "pf1": ["-DHX_SW_PK_PF=1"], "pf2": ["-DHX_SW_PK_PF=2"], "pkexp2": ["-DHX_SW_PK_EXP=2"],
             "swexp1": ["-DHX_SW_EXP=1"], "swexp2": ["-DHX_SW_EXP=2"], "swexp3": ["-DHX_SW_EXP=3"], "swexp4": ["-DHX_SW_EXP=4"],

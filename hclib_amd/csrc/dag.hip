@@ -190,14 +190,17 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
     std::vector<uint32_t> sat;
     if (datum_out && g_dag.npromises)
         HX_HIP(hipMemcpyAsync(datum_out, v.datum, (size_t)g_dag.npromises * 8, hipMemcpyDeviceToHost, m.stream));
-    if (satisfied_out && g_dag.npromises) {
+    // always read back: tagged puts count `satisfied` up without a result,
+    // so a double put shows only here (a count of 2), whether or not the
+    // caller asked for the satisfied flags
+    if (g_dag.npromises) {
         sat.resize(g_dag.npromises);
         HX_HIP(hipMemcpyAsync(sat.data(), v.satisfied, sat.size() * 4, hipMemcpyDeviceToHost, m.stream));
     }
     HX_HIP(hipStreamSynchronize(m.stream));
     bool twice = false;  // tagged puts count satisfied up (hx_dag.h kTagged): 2 = put twice
     for (size_t p = 0; p < sat.size(); ++p) {
-        satisfied_out[p] = sat[p] ? 1 : 0;
+        if (satisfied_out) satisfied_out[p] = sat[p] ? 1 : 0;
         twice = twice || sat[p] > 1;
     }
     if (twice && !err) err = kErrDoublePut;

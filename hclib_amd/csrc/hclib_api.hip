@@ -78,6 +78,7 @@ struct Runtime {
     };
     std::map<int, MemFuncs> mem;
     bool mem_builtins = false;
+    double user_timer = 0.0;  // hclib_user_harness_timer
     // stats (HCLIB_STATS analogue, src/hclib-runtime.c:83-104)
     unsigned long long host_tasks = 0, device_tasks = 0, end_finishes = 0, forasyncs = 0;
     unsigned long long spawned = 0, future_waits = 0, end_finishes_nb = 0, yields = 0, yield_iters = 0;
@@ -966,6 +967,42 @@ extern "C" {
 // tasks live in the megakernel's queues only while a launch runs.
 size_t hclib_current_worker_backlog(void) { return rt().ready.size(); }
 
+// src/hclib-locality-graph.c:760-768: tasks queued at `locale` over every
+// worker's deque there. Here: the ready host tasks placed at it (a task
+// spawned without a locale sits at the closest locale, the reference's
+// default push place, src/hclib-runtime.c:518-521)
+unsigned locale_num_tasks(hclib_locale_t *locale) {
+    if (!locale) die("locale_num_tasks: NULL locale");
+    hclib_locale_t *dflt = hclib_get_closest_locale();
+    unsigned n = 0;
+    for (hclib_task_t *t : rt().ready) n += (t->locale ? t->locale : dflt) == locale;
+    return n;
+}
+
+// src/hclib-locality-graph.c:807-813: append to the locale's idle functions
+void locale_register_idle_task(hclib_locale_t *locale, void (*fp)(void)) {
+    if (!locale || !fp) die("locale_register_idle_task: NULL argument");
+    void (**grown)(void) =
+        (void (**)(void))realloc((void *)locale->idle_funcs, (locale->n_idle_funcs + 1) * sizeof(void (*)(void)));
+    if (!grown) die("locale_register_idle_task: out of memory");
+    locale->idle_funcs = grown;
+    locale->idle_funcs[locale->n_idle_funcs++] = fp;
+}
+
+// src/hclib-locality-graph.c:815-827: every idle function of every locale on
+// the worker's steal path, in path order
+void locale_run_idle_tasks(hclib_worker_state *ws) {
+    if (!ws || !ws->paths || !ws->paths->steal_path) die("locale_run_idle_tasks: worker has no paths");
+    const hclib_locality_path *steal = ws->paths->steal_path;
+    for (unsigned i = 0; i < steal->path_length; ++i) {
+        hclib_locale_t *l = steal->locales[i];
+        for (unsigned j = 0; j < l->n_idle_funcs; ++j) l->idle_funcs[j]();
+    }
+}
+
+// src/hclib-runtime.c:1319-1321: recorded; HCLIB_STATS prints it
+void hclib_user_harness_timer(double dur) { rt().user_timer = dur; }
+
 // src/hclib-runtime.c:480-486: used / capacity of the caller's deque
 void hclib_default_queue_capacity(int *used, int *capacity) {
     if (used) *used = (int)rt().ready.size();
@@ -1015,12 +1052,21 @@ hclib_locale_t *hclib_hip_gpu_locale(int index) {
     // (or without the hip module loaded) fails here, loudly
     if (hxh::gpu_type() == ~0u)
         die("hclib_hip_gpu_locale: no GPU locale type (load the \"hip\" module: deps {\"system\", \"hip\"})");
-    ensure_gpu("hclib_hip_gpu_locale", index);
+    // the locale first: a graph without this device (e.g. LOCAL_RANK=1's,
+    // which holds only GPU 1) must not initialise the device before failing
     const int n = hclib_get_num_locales();
+    bool any_gpu = false;
     for (int i = 0; i < n; ++i) {
         hclib_locale_t *l = hclib_get_locale(i);
-        if (hxh::locale_device(l) == index) return l;
+        any_gpu = any_gpu || hxh::locale_device(l) >= 0;
+        if (hxh::locale_device(l) == index) {
+            ensure_gpu("hclib_hip_gpu_locale", hxh::locale_device(l));
+            return l;
+        }
     }
+    // a graph without any GPU: the module found no device to bind; say why
+    // (binding is what failed, and no other GPU of the graph gets touched)
+    if (!any_gpu) ensure_gpu("hclib_hip_gpu_locale", index);
     die("hclib_hip_gpu_locale: the locality graph has no locale for GPU %d", index);
 }
 
@@ -1109,6 +1155,7 @@ void hclib_print_runtime_stats(FILE *fp) {
             "0 ctx creates, %llu yields, %f iters per yield on average\n",
             R.host_tasks + R.device_tasks + dev_exec, R.end_finishes, R.future_waits, R.end_finishes_nb,
             R.yields, R.yields ? (double)R.yield_iters / (double)R.yields : 0.0);
+    if (R.user_timer > 0.0) fprintf(fp, "User harness timer: %f s\n", R.user_timer);
 }
 
 }  // extern "C"

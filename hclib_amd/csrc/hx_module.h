@@ -34,6 +34,10 @@ struct Module {
     // cross-GPU work sharing (hclib_hip_global_attach): the shared region's
     // view for sharded launches, hdr null while detached
     GlobalView gview = {nullptr, nullptr, nullptr, 0, 0};
+    // diagnostic worker timelines (HX_TIMELINE builds, HCLIB_HIP_TIMELINE=<events per worker>)
+    unsigned long long *timeline = nullptr;
+    uint32_t timeline_cap = 0;
+    std::vector<unsigned long long> last_timeline;  // the last launch's, workers * timeline_cap
 };
 
 Module &mod();

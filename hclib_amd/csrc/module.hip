@@ -149,6 +149,19 @@ int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global) {
     init.wave_stats = m.wave_stats;
     init.wave_stats_cap = m.wave_stats_cap;
     if (global) init.gview = m.gview;
+    // diagnostic timelines: only a HX_TIMELINE build writes them
+    const int tl_cap = env_int("HCLIB_HIP_TIMELINE", 0);
+    if (tl_cap > 0) {
+        if (!m.timeline || (uint32_t)tl_cap != m.timeline_cap) {
+            if (m.timeline) (void)hipFree(m.timeline);
+            m.timeline = nullptr;
+            HX_HIP(hipMalloc((void **)&m.timeline, (size_t)m.wave_stats_cap * tl_cap * 8));
+            m.timeline_cap = (uint32_t)tl_cap;
+        }
+        HX_HIP(hipMemsetAsync(m.timeline, 0, (size_t)m.wave_stats_cap * tl_cap * 8, m.stream));
+        init.timeline = m.timeline;
+        init.timeline_cap = m.timeline_cap;
+    }
     // a pinned staging copy of its own, reused: every launch ends with the
     // stream synchronised (hclib_hip_sched_end), so the last copy is done
     static SchedGlobals *stage = nullptr;
@@ -184,6 +197,14 @@ int finish_sched(SchedGlobals *host_copy, const char *who) {
     if (nw > nw_cap) nw = nw_cap;
     m.last_waves.resize(nw);
     if (nw) HX_HIP(hipMemcpy(m.last_waves.data(), m.wave_stats, nw * sizeof(WaveStat), hipMemcpyDeviceToHost));
+    if (host_copy->timeline) {
+        m.last_timeline.resize((size_t)nw * m.timeline_cap);
+        if (nw)
+            HX_HIP(hipMemcpy(m.last_timeline.data(), m.timeline, (size_t)nw * m.timeline_cap * 8,
+                             hipMemcpyDeviceToHost));
+    } else {
+        m.last_timeline.clear();
+    }
     if (host_copy->err) {
         set_error("%s: device error %u (%s)", who, host_copy->err, err_name(host_copy->err));
         return HCLIB_HIP_EDEVICE;
@@ -241,6 +262,7 @@ void hclib_hip_finalize(void) {
     if (m.pool_mem) (void)hipFree(m.pool_mem);
     (void)hipFree(m.globals);
     (void)hipFree(m.wave_stats);
+    if (m.timeline) (void)hipFree(m.timeline);
     (void)hipEventDestroy(m.ev0);
     (void)hipEventDestroy(m.ev1);
     (void)hipStreamDestroy(m.stream);
@@ -266,6 +288,14 @@ int hclib_hip_last_wave_stats(hclib_hip_wave_stats_t *out, int max) {
     const int n = (int)g_mod.last_waves.size();
     for (int i = 0; out && i < n && i < max; ++i) memcpy(&out[i], &g_mod.last_waves[(size_t)i], sizeof(WaveStat));
     return n;
+}
+
+int hclib_hip_last_timeline(uint64_t *out, uint64_t max_words, uint32_t *events_per_worker) {
+    Module &m = g_mod;
+    if (events_per_worker) *events_per_worker = m.last_timeline.empty() ? 0u : m.timeline_cap;
+    const uint64_t n = m.last_timeline.size();
+    for (uint64_t i = 0; out && i < n && i < max_words; ++i) out[i] = m.last_timeline[i];
+    return m.timeline_cap ? (int)(n / m.timeline_cap) : 0;
 }
 
 int hclib_hip_sched_begin(uint32_t entry_words, uint32_t chunk, int waves_per_cu,

@@ -1360,10 +1360,15 @@ __host__ __device__ constexpr int sw_pk_lds_words(int tw) {
 inline size_t sw_pk_lds_bytes(int tw) { return (size_t)sw_pk_lds_words(tw) * 4; }
 
 // wait until an LDS counter reaches `want` (bounded; device error on timeout)
+// EQ: wait for the flag to equal `want` (a per-tile flag whose tiles are not
+// monotone per workgroup: tile (1, 0) is id ntw and tile (0, 2) may run after
+// it); otherwise for it to reach `want` (counters that only grow)
+template <bool EQ = false>
 __device__ __forceinline__ bool sw_pk_wait(const SwCtx &c, const int *flag, int want) {
-    if (lds_flag_ld(flag) >= want) return true;
+    auto done = [&]() { return EQ ? lds_flag_ld(flag) == want : lds_flag_ld(flag) >= want; };
+    if (done()) return true;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t n = 1; lds_flag_ld(flag) < want; ++n) {
+    for (uint32_t n = 1; !done(); ++n) {
         __builtin_amdgcn_s_sleep(1);
         if ((n & 255) == 0) {
             if (ld_agent(c.err)) return false;
@@ -1671,7 +1676,7 @@ struct SwDagPkKind {
         if (wave == 2) {
             // run_dag_group's helper (the workgroup's last wave): returns once
             // the tile's LDS outputs (the corner datum) exist
-            return sw_pk_wait(c, &misc[4], (int)t + 1);
+            return sw_pk_wait<true>(c, &misc[4], (int)t + 1);
         }
         if (wave == 1) {
             int *tbl = misc + kSwPkMisc;

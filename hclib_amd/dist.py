@@ -11,7 +11,9 @@ same code runs on "gloo" for the CPU tests.
 """
 from __future__ import annotations
 
+import datetime
 import os
+import threading
 
 
 def init_from_env(backend: str = "nccl", share_device: bool = False):
@@ -31,16 +33,89 @@ def init_from_env(backend: str = "nccl", share_device: bool = False):
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # a bounded rendezvous / collective timeout (HCLIB_DIST_TIMEOUT_S,
+        # default 300 s): a rank that never arrives fails the job instead of
+        # hanging it for torch's default; RCCL collectives that time out then
+        # raise in the waiting rank (async error handling 2: abort the
+        # communicator, keep the process) rather than killing it
+        timeout = datetime.timedelta(seconds=int(os.environ.get("HCLIB_DIST_TIMEOUT_S", "300")))
         if backend == "nccl":
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
             torch.cuda.set_device(dev)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev), timeout=timeout)
         else:
             if share_device:
                 torch.cuda.set_device(dev)
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
     elif backend == "nccl":
         torch.cuda.set_device(dev)
     return rank, world, local
+
+
+class LegGuard:
+    """Wall-clock guard for the optional legs of a multi-rank run (bench.py's
+    N > 1 extras: sharded triad, sharded SW, cross-GPU work sharing). Each leg
+    runs in a worker thread; a leg with no result after `timeout_s` is
+    reported as failed and marks the job stalled in the rendezvous store
+    (served by rank 0's process, so it answers while any rank's main thread
+    is blocked), after which every rank skips the remaining legs. A leg that
+    raises is reported with its exception. The caller prints its line and,
+    when `stalled`, leaves with os._exit (a blocked collective thread would
+    hold a normal shutdown)."""
+
+    KEY = "hclib_leg_stalled"
+
+    def __init__(self, world: int, timeout_s: float, device: int | None = None, store=None):
+        self.world, self.timeout_s, self.device = world, timeout_s, device
+        self.stalled = False
+        self.store = store
+        if self.store is None and world > 1:
+            import torch.distributed as dist
+
+            try:
+                self.store = dist.distributed_c10d._get_default_store()
+            except Exception:  # noqa: BLE001 (no store: each rank only knows its own stalls)
+                self.store = None
+
+    def _peer_stalled(self) -> bool:
+        if self.store is None:
+            return False
+        try:
+            return bool(self.store.check([self.KEY]))
+        except Exception:  # noqa: BLE001
+            return False
+
+    def run(self, name: str, fn):
+        """fn() -> dict; returns its result or {"failed": reason}."""
+        if self.stalled or self._peer_stalled():
+            self.stalled = True
+            return {"failed": "skipped: an earlier leg stalled on some rank"}
+        box = {}
+
+        def target():
+            try:
+                if self.device is not None:
+                    import torch
+
+                    torch.cuda.set_device(self.device)
+                box["r"] = fn()
+            except BaseException as e:  # noqa: BLE001 (SystemExit from a mismatch included)
+                box["e"] = f"{type(e).__name__}: {e}"
+
+        th = threading.Thread(target=target, name=f"leg-{name}", daemon=True)
+        th.start()
+        th.join(self.timeout_s)
+        if th.is_alive():
+            self.stalled = True
+            if self.store is not None:
+                try:
+                    self.store.set(self.KEY, name)
+                except Exception:  # noqa: BLE001
+                    pass
+            return {"failed": f"timeout: no result after {self.timeout_s:g} s (wall-clock guard)"}
+        if "e" in box:
+            return {"failed": box["e"]}
+        return box["r"]
 
 
 def _device(backend: str):

@@ -83,6 +83,15 @@ int hclib_get_num_locales_of_type(int locale_type);
 
 unsigned hclib_add_known_locale_type(const char *lbl);
 
+/* inc/hclib-locality-graph.h:102-105 (src/hclib-locality-graph.c:760-829):
+ * tasks queued at a locale (here: ready host tasks placed there — the host
+ * control thread is this build's one host worker; device tasks live in the
+ * megakernel's queues only while a launch runs), and per-locale idle
+ * functions, run for every locale of a worker's steal path on request */
+unsigned locale_num_tasks(hclib_locale_t *locale);
+void locale_run_idle_tasks(hclib_worker_state *ws);
+void locale_register_idle_task(hclib_locale_t *locale, void (*fp)(void));
+
 #ifdef __cplusplus
 }
 #endif

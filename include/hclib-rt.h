@@ -80,6 +80,9 @@ typedef void (*generic_frame_ptr)(void *);
 int hclib_get_num_workers(void);
 void hclib_start_finish(void);
 void hclib_end_finish(void);
+/* inc/hclib-rt.h:153 (src/hclib-runtime.c:1319-1321): the harness's own
+ * timing of the user region, in seconds; HCLIB_STATS reports it */
+void hclib_user_harness_timer(double dur);
 
 #ifdef __cplusplus
 }

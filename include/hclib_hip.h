@@ -94,6 +94,12 @@ int hclib_hip_last_wave_stats(hclib_hip_wave_stats_t *out, int max);
 /* The narrow-frontier carry loop of the last launch (hx_sched.h): [0]
  * batches run in it, [1] shader-clock cycles spent in it, [2] entries. */
 void hclib_hip_last_narrow_counters(uint64_t out[4]);
+/* Worker timelines of the last megakernel launch (diagnostic: a library
+ * built with `--variant timeline` and HCLIB_HIP_TIMELINE=<events per
+ * worker>; hx_sched.h Timeline). Copies at most `max_words` events (worker w's
+ * at [w * events_per_worker ...], 0 = unused) and returns the worker count
+ * (0 when no timeline was recorded). */
+int hclib_hip_last_timeline(uint64_t *out, uint64_t max_words, uint32_t *events_per_worker);
 
 /* L2 atomic-throughput calibration: the saturated rate (million atomic
  * ops per second, whole GPU) of one access shape the runtime's atomics use,

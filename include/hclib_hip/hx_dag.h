@@ -350,7 +350,9 @@ struct group_tagged<K, decltype((void)K::kTagged)> { static constexpr bool value
 // kDagSkip (kept, or not released). The put's other releases then reach the
 // ready list one round trip sooner than through the helper's append at the
 // next task; the list holds view.nslots entries (hclib_hip_dag_begin), and
-// tickets run to that count. Needs at most 64 waiter entries per task.
+// tickets run to that count. Waiter lists of more than 64 entries per task
+// take the same reserved form 64 entries at a time (not prefetched). Only
+// tagged Kinds may reserve (static_assert in run_dag_group).
 template <class K, class = void>
 struct group_reserve { static constexpr bool value = false; };
 template <class K>
@@ -399,6 +401,10 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
     constexpr bool kTagged = group_tagged<Kind>::value;
     constexpr bool kReserve = group_reserve<Kind>::value;
     static_assert(!kReserve || N > 0, "reserved puts use the split put");
+    // a reserved put counts `satisfied` up (no exchange to wait for), so its
+    // double puts are found by hclib_hip_dag_end like a tagged Kind's: only
+    // tagged Kinds may reserve
+    static_assert(!kReserve || kTagged, "reserved puts need a tagged Kind");
     const uint32_t nslots = kReserve ? view.nslots : view.ntasks;
     static_assert(!kTagged || (N > 0 && Kind::kSc1Payload), "tagged puts use the split put of sc1 payloads");
     __shared__ DagGroupShared sh;
@@ -587,17 +593,66 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
             if (wave == 0) {
                 const uint32_t nwait = sh.nwait;
                 if (nwait > 64) {
-                    // (reserved puts need <= 64 waiter entries: the ordinary put
-                    // below appends releases only, so the slot count would be off)
-                    if (kReserve && lane == 0) dev_error(view.err, kErrBadTask);
                     uint32_t p[N];
                     unsigned long long d[N];
                     Kind::promises(ctx, t, p);
                     Kind::datums(ctx, t, d);
-                    // long waiter lists: the ordinary batched put (it appends
-                    // its releases itself)
-                    dag_put_n<N, Kind::kSc1Payload>(w, p, d);
-                    if (w.next != kDagEmpty && lane == w.skip_lane) st_agent(&view.ready[w.skip_pos], kDagSkip);
+                    if constexpr (kReserve) {
+                        // long waiter lists (not prefetched, so the helper did not
+                        // publish): the datums and satisfied counts here, then
+                        // the reserved release 64 waiter entries at a time, all
+                        // nwait slots taken with one tail fetch-add
+                        uint32_t my_p = 0;
+                        unsigned long long my_d = 0;
+#pragma unroll
+                        for (int i = 0; i < N; ++i)
+                            if (lane == i) {
+                                my_p = p[i];
+                                my_d = d[i];
+                            }
+                        if (lane < N) {
+                            st_agent(&view.datum[my_p], my_d);
+                            __hip_atomic_fetch_add(&view.satisfied[my_p], 1u, __ATOMIC_RELAXED, HX_AGENT);
+                        }
+                        uint32_t base = 0;
+                        if (lane == 0) base = add_agent(view.tail, nwait);
+                        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+                        // a put past the reserved slots (a promise put twice):
+                        // no release, no ready write, a device error
+                        const bool fits = base + nwait <= nslots;
+                        if (!fits && lane == 0) dev_error(view.err, kErrDoublePut);
+                        uint32_t off = 0, rel = 0;
+#pragma unroll
+                        for (int i = 0; i < N; ++i) {
+                            const uint32_t bi = view.waiter_off[p[i]], ei = view.waiter_off[p[i] + 1];
+                            for (uint32_t k0 = bi; fits && k0 < ei; k0 += 64) {
+                                const uint32_t k = k0 + (uint32_t)lane;
+                                uint32_t rt = kDagEmpty;
+                                if (k < ei) {
+                                    const uint32_t c = view.waiters[k];
+                                    if (add_agent(&view.deps[c], (uint32_t)-1) == 1u) rt = c;
+                                }
+                                const unsigned long long m = __ballot(rt != kDagEmpty);
+                                int kept_lane = -1;
+                                if (m && w.next == kDagEmpty) {
+                                    kept_lane = __builtin_ctzll(m);
+                                    w.next = (uint32_t)__builtin_amdgcn_readlane((int)rt, kept_lane);
+                                }
+                                if (k < ei)
+                                    st_agent(&view.ready[base + off + (k - bi)],
+                                             (rt != kDagEmpty && lane != kept_lane) ? rt : kDagSkip);
+                                rel += (uint32_t)__builtin_popcountll(m);
+                            }
+                            off += ei - bi;
+                        }
+                        w.puts += N;
+                        w.releases += rel;
+                    } else {
+                        // long waiter lists: the ordinary batched put (it appends
+                        // its releases itself)
+                        dag_put_n<N, Kind::kSc1Payload>(w, p, d);
+                        if (w.next != kDagEmpty && lane == w.skip_lane) st_agent(&view.ready[w.skip_pos], kDagSkip);
+                    }
                     if (lane == 0) {
                         sh.npend = 0;
                         sh.skip = 0;
@@ -617,13 +672,18 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
 #endif
                     }
                     base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-                    const unsigned long long m = __ballot(rt != kDagEmpty);
+                    // a put past the reserved slots (a promise put twice, which
+                    // tagged puts otherwise report only after the launch): no
+                    // ready write beyond the list, a device error at once
+                    const bool fits = base + nwait <= nslots;
+                    if (!fits && lane == 0) dev_error(view.err, kErrDoublePut);
+                    const unsigned long long m = fits ? __ballot(rt != kDagEmpty) : 0ull;
                     int kept_lane = -1;
                     if (m) {  // keep the first released task (see dag_put_one)
                         kept_lane = __builtin_ctzll(m);
                         w.next = (uint32_t)__builtin_amdgcn_readlane((int)rt, kept_lane);
                     }
-                    if ((uint32_t)lane < nwait)
+                    if (fits && (uint32_t)lane < nwait)
                         st_agent(&view.ready[base + (uint32_t)lane], (rt != kDagEmpty && lane != kept_lane) ? rt : kDagSkip);
                     if (lane == 0) {
                         sh.npend = 0;

@@ -52,10 +52,15 @@ namespace hx {
 
 constexpr int kWaveSize = 64;
 
-// One HBM chunk deque header, head and tail on separate 128-B lines.
+// One HBM chunk deque header, head and tail on separate 128-B lines. `done`
+// shares the head's 8 bytes: the wave that ends the launch (its decrement
+// takes `outstanding` to 0) sets it in every header, so an idle wave learns
+// of termination from the head load of its next probe instead of polling the
+// one `outstanding` line that every busy wave's spills and hunger reads use.
 struct alignas(256) QueueHdr {
     uint32_t head;
-    uint32_t pad0[31];
+    uint32_t done;
+    uint32_t pad0[30];
     uint32_t tail;
     uint32_t pad1[31];
 };
@@ -119,8 +124,11 @@ struct GlobalView {
 struct alignas(256) SchedGlobals {
     uint32_t outstanding;  // chunks queued + waves holding work
     uint32_t pad0[63];
-    uint32_t hint;  // deque most recently pushed to
+    uint32_t hint;  // (unused; per-XCD hints below)
     uint32_t pad1[63];
+    // per XCD x, hints[64 x]: the deque most recently pushed to in x's slice
+    // (eight lines, so idle waves' hint reads do not all hit one line)
+    uint32_t hints[8 * 64];
     uint32_t err;  // DevError
     uint32_t pad2[63];
     unsigned long long counters[16];  // [0..7] kind-specific, [8..15] scheduler
@@ -129,6 +137,48 @@ struct alignas(256) SchedGlobals {
     uint32_t wave_stats_cap;          // records available
     unsigned long long narrow[4];     // narrow-frontier loop: [0] batches, [1] s_memtime cycles, [2] entries
     GlobalView gview;                 // cross-GPU work sharing (gview.hdr null: off)
+    // diagnostic timeline (HX_TIMELINE builds, HCLIB_HIP_TIMELINE=1): per
+    // worker `timeline_cap` events of lane 0 (see Timeline), or null
+    unsigned long long *timeline;
+    uint32_t timeline_cap;
+};
+
+// Diagnostic build (-DHX_TIMELINE=1, `python -m hclib_amd.build --variant
+// timeline`): every worker logs its transitions — start, busy (work taken),
+// idle, chunk given away, termination seen, exit — as
+// s_memrealtime (100 MHz) << 24 | type << 20 | value (20 bits), so the host
+// can draw the active-worker count against time (scripts/uts_timeline.py).
+// Transitions are rare (never per batch), so the log costs the search
+// little; the product build compiles it out.
+#ifndef HX_TIMELINE
+#define HX_TIMELINE 0
+#endif
+enum : uint32_t {
+    kTlStart = 1,  // value: 0
+    kTlBusy = 2,   // value: items taken | source << 16 (0 roots, 1 home deque, 2 other deque, 3 inbox, 4 global)
+    kTlIdle = 3,   // value: 0
+    kTlSpill = 4,  // value: items given away (a chunk or an inbox)
+    kTlTerm = 5,   // value: 0 — this worker saw the launch's termination
+    kTlEnd = 6,    // value: 0 — after the exit reductions
+};
+struct Timeline {
+    unsigned long long *p;
+    uint32_t n, cap;
+    __device__ __forceinline__ void init(SchedGlobals *g, uint32_t worker) {
+#if HX_TIMELINE
+        cap = g->timeline_cap;
+        p = g->timeline ? g->timeline + (size_t)worker * cap : nullptr;
+        n = 0;
+#endif
+    }
+    __device__ __forceinline__ void log(uint32_t type, uint32_t value) {
+#if HX_TIMELINE
+        if (p && n < cap && lane_id() == 0)
+            p[n] = ((unsigned long long)__builtin_amdgcn_s_memrealtime() << 24) | ((unsigned long long)type << 20) |
+                   (value & 0xfffffu);
+        ++n;
+#endif
+    }
 };
 
 // Diagnostic build (-DHX_STAMPS=1): per-phase s_memtime stamps, enabled at run
@@ -367,7 +417,7 @@ __device__ __forceinline__ void publish_pending(const PoolView &pool, SchedGloba
     handoff_publish();  // the payload + cnt stores are complete
     if (lane_id() == 0) {
         st_agent(slot_ctl(pool, pc.slot), pc.pos + 1);
-        st_agent(&g->hint, pc.q);
+        st_agent(&g->hints[64u * ((pc.q / (pool.nq / 8u)) & 7u)], pc.q);
     }
     pc.live = false;
 }
@@ -400,10 +450,12 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
             seen = tl - hd;
             // a ring-full relief may fill the deque to its last slot: a ticket
             // below head + cap waits only for a consumer that already claimed
-            // the previous lap's ticket (no deadlock, a short bounded wait)
-            if ((int)(tl - hd) < (int)(relief ? pool.cap - 1 : pool.cap / 2)) {
-                add_agent(&g->outstanding, 1u);
-                pos = add_agent(&h->tail, 1u);
+            // the previous lap's ticket (no deadlock, a short bounded wait).
+            // The ticket is taken by CAS on the tail it checked, so concurrent
+            // producers cannot together push it past that bound
+            if ((int)(tl - hd) < (int)(relief ? pool.cap - 1 : pool.cap / 2) && cas_agent(&h->tail, tl, tl + 1u)) {
+                add_agent(&g->outstanding, 1u);  // before the chunk is published
+                pos = tl;
                 ok = 1;
             }
         }
@@ -446,7 +498,7 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
     handoff_publish();
     if (lane == 0) {
         st_agent(slot_ctl(pool, slot), pos + 1);
-        st_agent(&g->hint, q);
+        st_agent(&g->hints[64u * ((q / (pool.nq / 8u)) & 7u)], q);
     }
     // nothing stays in flight past a spill (see vm_drain)
     vm_drain();
@@ -457,22 +509,26 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
 // number of entries taken (0 if the deque looked empty). Round trips: the
 // head/tail read, the head CAS, the {seq, cnt} pair, the payload; the slot
 // is handed back with a store nobody waits for.
+// `done` (wave-uniform) receives the header's termination flag.
 template <class Kind, int CAP>
 __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Kind, CAP> &st,
-                                  SchedGlobals *g) {
+                                  SchedGlobals *g, uint32_t &done) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     QueueHdr *h = &pool.hdr[q];
-    uint32_t pos = 0;
+    uint32_t pos = 0, fin = 0;
     int ok = 0;
     if (lane == 0) {
         // one claim attempt: a ticket below the tail, taken by CAS on the head
-        const uint32_t hd = ld_agent(&h->head), tl = ld_agent(&h->tail);
+        const unsigned long long hd2 = ld_agent((const unsigned long long *)&h->head);
+        const uint32_t hd = (uint32_t)hd2, tl = ld_agent(&h->tail);
+        fin = (uint32_t)(hd2 >> 32);
         if ((int)(tl - hd) > 0 && cas_agent(&h->head, hd, hd + 1)) {
             pos = hd;
             ok = 1;
         }
     }
+    done = lane0(fin);
     if (!lane0((uint32_t)ok)) return 0;
     pos = lane0(pos);
     const uint32_t slot = q * pool.cap + (pos & (pool.cap - 1));
@@ -971,7 +1027,7 @@ __device__ uint32_t inbox_take(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st) {
 // a wave stops holding work: local `outstanding` -1; the wave that takes it
 // to 0 releases its rank's unit of the global `active` (GLOBAL launches)
 template <bool GLOBAL>
-__device__ __forceinline__ void wave_goes_idle(SchedGlobals *g, const GlobalView &gv) {
+__device__ __forceinline__ void wave_goes_idle(SchedGlobals *g, const GlobalView &gv, const PoolView &pool) {
     if (lane_id() != 0) return;
     if constexpr (GLOBAL) {
         const uint32_t prev = __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
@@ -983,7 +1039,12 @@ __device__ __forceinline__ void wave_goes_idle(SchedGlobals *g, const GlobalView
             add_sys(&gv.hdr->active, (uint32_t)-1);
         }
     } else {
-        __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+        const uint32_t prev = __hip_atomic_fetch_add(&g->outstanding, (uint32_t)-1, __ATOMIC_RELEASE, HX_AGENT);
+        if (prev == 1u) {
+            // no wave holds work and no chunk is queued: that is final (only
+            // holders create work), so tell every deque's pollers
+            for (uint32_t q = 0; q < pool.nq; ++q) st_agent(&pool.hdr[q].done, 1u);
+        }
     }
 }
 
@@ -1017,6 +1078,9 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
 
     typename Kind::Acc acc;
     acc_set_wid(acc, gid);
+    Timeline tl;
+    tl.init(g, gid);
+    tl.log(kTlStart, 0);
     uint32_t bot = 0, top = 0;
     bool active = false;
     uint32_t spins = 0;
@@ -1057,9 +1121,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         tag += 16;
         top = tout;
         active = true;  // the host initialised outstanding = 1 for this wave
+        tl.log(kTlBusy, tout);
         if (top == 0) {
             active = false;
-            wave_goes_idle<GLOBAL>(g, gv);
+            wave_goes_idle<GLOBAL>(g, gv, pool);
         }
     }
 
@@ -1094,28 +1159,45 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             }
             if (active) {
                 active = false;
-                wave_goes_idle<GLOBAL>(g, gv);
+                wave_goes_idle<GLOBAL>(g, gv, pool);
+                tl.log(kTlIdle, 0);
                 if constexpr (WPG > 1) {
                     if (lane == 0) *(volatile uint32_t *)&ib[wave].idle = 1u;
                 }
             }
-            // probe order: home, hint, then random (3/4 same XCD, 1/4 anywhere)
+            // probe order: home, a hint (the last deque pushed in an XCD's
+            // slice: this wave's own XCD first, then the others in turn), then
+            // random (3/4 same XCD, 1/4 anywhere)
             uint32_t q = home;
             const uint32_t phase = spins % 3;
             if (phase == 1) {
                 uint32_t hq = 0;
-                if (lane == 0) hq = ld_agent(&g->hint);
+                if (lane == 0) hq = ld_agent(&g->hints[64u * ((xcc + spins / 3u) & 7u)]);
                 q = lane0(hq) % pool.nq;
             } else if (phase == 2) {
                 uint32_t r = lane0(xorshift(rng));
                 q = ((r & 3) != 0) ? xcc * qpx + (r >> 2) % qpx : (r >> 2) % pool.nq;
             }
-            uint32_t n = 0;
+            uint32_t n = 0, src = 0;
             if constexpr (WPG > 1) {
                 n = inbox_take<Kind, CAP>(ib[wave], st);  // inherits the chunk's unit
-                if (n) q = home;
+                if (n) {
+                    q = home;
+                    src = 3;
+                }
             }
-            if (n == 0) n = dequeue_chunk<Kind, CAP>(pool, q, st, g);
+            uint32_t fin = 0;
+            if (n == 0) {
+                n = dequeue_chunk<Kind, CAP>(pool, q, st, g, fin);
+                src = q == home ? 1 : 2;
+            }
+            if constexpr (!GLOBAL) {
+                // the launch's last holder flagged every deque (wave_goes_idle)
+                if (fin) {
+                    tl.log(kTlTerm, 0);
+                    break;
+                }
+            }
             if constexpr (WPG > 1) {
                 if (n && lane == 0) *(volatile uint32_t *)&ib[wave].idle = 0u;
             }
@@ -1149,10 +1231,14 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                         }
                         add_sys(&gv.hdr->active, (uint32_t)-1);
                     }
-                    if (n) q = home;  // (not counted as a local steal)
+                    if (n) {
+                        q = home;  // (not counted as a local steal)
+                        src = 4;
+                    }
                 }
             }
             if (n) {
+                tl.log(kTlBusy, n | src << 16);
                 if (q != home) {
                     ++nsteal;
                     items_stolen += n;
@@ -1169,10 +1255,13 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 busy_phase = true;
                 continue;
             }
-            // termination / error check every 8th probe: `outstanding` is one
-            // line that every idle wave would otherwise poll, and the busy
-            // waves' hunger reads queue behind those polls
-            if ((spins & 7) == 7) {
+            // termination / error check: `outstanding` is one line that every
+            // idle wave would otherwise poll, and the busy waves' spills and
+            // hunger reads queue behind those polls. A local launch learns of
+            // its end from the deque headers (above) and reads the two words
+            // only every 64th probe (the error word, and a backstop); a
+            // sharing launch (GLOBAL) every 8th, its end being another count
+            if ((spins & (GLOBAL ? 7u : 63u)) == (GLOBAL ? 7u : 63u)) {
                 uint32_t outst = 0, e = 0;
                 if (lane == 0) {
                     outst = ld_agent(&g->outstanding);
@@ -1181,13 +1270,18 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 vm_drain();  // both loads land on every path (no phantom waits in the batch loop)
                 if (lane0(e)) break;
                 if (lane0(outst) == 0) {
-                    if constexpr (!GLOBAL) break;
-                    else {
+                    if constexpr (!GLOBAL) {
+                        tl.log(kTlTerm, 0);
+                        break;
+                    } else {
                         // no local work: the launch ends when no rank holds any
                         uint32_t ga = 0;
                         if (lane == 0) ga = ld_sys(&gv.hdr->active);
                         vm_drain();
-                        if (lane0(ga) == 0) break;
+                        if (lane0(ga) == 0) {
+                            tl.log(kTlTerm, 0);
+                            break;
+                        }
                     }
                 }
                 if constexpr (GLOBAL) {
@@ -1272,6 +1366,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     continue;
                 }
                 ++npush;
+                tl.log(kTlSpill, n);
                 bot += n;
             }
             return (top - bot) + tout <= kRoom;
@@ -1478,6 +1573,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 }
                 if (!ok) break;  // deques full: keep the items (the ring still has room)
                 ++npush;
+                tl.log(kTlSpill, n);
                 bot += n;
                 sz = top - bot;
                 if (hungry) --hungry;
@@ -1519,7 +1615,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                              cyc_narrow = st.cyc[3], t_begin = st.cyc[4], rt_begin = st.cyc[5];
     if (active) {
         // only reached on an error break: keep the protocol consistent
-        wave_goes_idle<GLOBAL>(g, gv);
+        wave_goes_idle<GLOBAL>(g, gv, pool);
     }
     acc.flush(g);
     {
@@ -1563,6 +1659,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         add_agent(&g->counters[kCtrClockTicks], t_end - t_begin);
         add_agent(&g->counters[kCtrRealTicks], rt_end - rt_begin);
     }
+    tl.log(kTlEnd, 0);
 }
 
 }  // namespace hx

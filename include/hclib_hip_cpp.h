@@ -393,6 +393,13 @@ class dag;
 template <class Kind>
 int run_dag(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats = nullptr, int waves_per_cu = 4,
             uint32_t spin_limit_ms = 0);
+// The same with workgroup tasks (hx::run_dag_group): every task runs on all
+// `waves_per_group` waves of one workgroup (Kind::run_group), puts split
+// around the body (kPutN / promises / datums) and, for tagged Kinds,
+// reserved ready slots (kReserve; include/hclib_hip/hx_dag.h).
+template <class Kind>
+int run_dag_groups(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats = nullptr,
+                   int groups_per_cu = 1, int waves_per_group = 1, uint32_t spin_limit_ms = 0);
 
 // Host-side graph builder: the device counterpart of creating promises with
 // hclib_promise_create and tasks with hclib_async(fn, arg, futures, n).
@@ -433,6 +440,9 @@ class dag {
     template <class Kind>
     friend int run_dag(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats, int waves_per_cu,
                        uint32_t spin_limit_ms);
+    template <class Kind>
+    friend int run_dag_groups(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats, int groups_per_cu,
+                              int waves_per_group, uint32_t spin_limit_ms);
 
   private:
     uint32_t words_;
@@ -460,6 +470,32 @@ int run_dag(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats,
     g.sat_.assign(g.num_promises(), 0);
     hclib_hip_dag_stats_t local;
     return hclib_hip_dag_end("hclib::hip::run_dag", g.datum_.data(), g.sat_.data(), stats ? stats : &local);
+}
+
+template <class Kind>
+__global__ __launch_bounds__(1024) void k_run_dag_groups(typename Kind::Ctx ctx, hx::DagView v) {
+    hx::run_dag_group<Kind>(ctx, v, nullptr);
+}
+
+template <class Kind>
+int run_dag_groups(const typename Kind::Ctx &ctx, dag &g, hclib_hip_dag_stats_t *stats, int groups_per_cu,
+                   int waves_per_group, uint32_t spin_limit_ms) {
+    if (waves_per_group < 1 || waves_per_group > 16) {
+        fprintf(stderr, "hclib::hip::run_dag_groups: 1..16 waves per group\n");
+        return HCLIB_HIP_EINVAL;
+    }
+    hclib_hip_dag_launch_t L;
+    int rc = hclib_hip_dag_begin(g.num_tasks(), g.num_promises(), g.words_, g.payload_.data(), g.await_off_.data(),
+                                 g.await_ids_.data(), g.preput_.data(), g.pre_datum_.data(), groups_per_cu,
+                                 spin_limit_ms, &L);
+    if (rc != HCLIB_HIP_OK) return rc;
+    const hx::DagView v = *(const hx::DagView *)L.view;
+    hipLaunchKernelGGL((k_run_dag_groups<Kind>), dim3(L.grid), dim3(64 * waves_per_group), 0, (hipStream_t)L.stream,
+                       ctx, v);
+    g.datum_.assign(g.num_promises(), 0);
+    g.sat_.assign(g.num_promises(), 0);
+    hclib_hip_dag_stats_t local;
+    return hclib_hip_dag_end("hclib::hip::run_dag_groups", g.datum_.data(), g.sat_.data(), stats ? stats : &local);
 }
 
 // ------------------------------------------------- dynamic device dataflow

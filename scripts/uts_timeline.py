@@ -1,0 +1,108 @@
+"""Active-worker timelines of the UTS megakernel (diagnostic; VERDICT r03
+item 1). Runs on the `--variant timeline` library (hx_sched.h Timeline):
+
+    HCLIB_AMD_LIB=hclib_amd/lib/timeline/libhclib_amd.so \
+        python scripts/uts_timeline.py out.jsonl [T1 T1L T1XL:7]
+
+`T1XL:7` searches every shard of bench's 8-way partition at split depth 7
+(bench.py's N=8 wide-tree leg, one shard at a time). For each launch the line
+holds: the kernel time, when the workers started (launch ramp), when 10 / 50
+/ 90 % of them first held work, when the last work item was finished (the
+last busy -> idle), when the workers saw termination and left, and the
+active-worker count per time bin. Timeline launches run slower than the
+product build by their stores; quote the product build's times.
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("HCLIB_HIP_TIMELINE", "2048")
+import torch  # noqa: E402,F401
+import hclib_amd as H  # noqa: E402
+
+TREES = {"T1": ("-t 1 -a 3 -d 10 -b 4 -r 19", 4130071),
+         "T1L": ("-t 1 -a 3 -d 13 -b 4 -r 29", 102181082),
+         "T1XL": ("-t 1 -a 3 -d 15 -b 4 -r 29", 1635119272),
+         "T3L": ("-t 0 -b 2000 -q 0.200014 -m 5 -r 7", 111345631)}
+
+
+def summarise(tl, kernel_ms, bins=100):
+    starts = [e[0] for w in tl for e in w if e[1] == 1]
+    t0 = min(starts)
+    us = lambda t: (t - t0) / 100.0  # 100 MHz ticks -> us
+    first_busy, last_idle, terms, ends = [], [], [], []
+    intervals = []
+    spills = 0
+    for w in tl:
+        busy_since = None
+        for t, ev, val in w:
+            if ev == 2:
+                if busy_since is None:
+                    busy_since = t
+                if not first_busy or len(first_busy) < len(tl):
+                    pass
+            elif ev == 3 and busy_since is not None:
+                intervals.append((us(busy_since), us(t)))
+                last_idle.append(us(t))
+                busy_since = None
+            elif ev == 4:
+                spills += 1
+            elif ev == 5:
+                terms.append(us(t))
+            elif ev == 6:
+                ends.append(us(t))
+        fb = [us(t) for t, ev, _ in w if ev == 2]
+        first_busy.append(min(fb) if fb else None)
+    held = sorted(x for x in first_busy if x is not None)
+    nw = len(tl)
+    end = max(ends) if ends else max(last_idle)
+    width = end / bins
+    curve = [0.0] * bins
+    for a, b in intervals:  # worker-time inside each bin / bin width = mean active workers
+        i0, i1 = int(a / width), min(bins - 1, int(b / width))
+        for i in range(i0, i1 + 1):
+            lo, hi = max(a, i * width), min(b, (i + 1) * width)
+            if hi > lo:
+                curve[i] += (hi - lo) / width
+    pct = lambda f: held[min(len(held) - 1, int(f * nw))] if len(held) > f * nw else None
+    busy_us = sum(b - a for a, b in intervals)
+    return {
+        "kernel_ms": kernel_ms, "workers": nw, "workers_that_held_work": len(held),
+        "start_spread_us": us(max(starts)),
+        "first_work_us": {"10%": pct(0.1), "50%": pct(0.5), "90%": pct(0.9)},
+        "last_item_done_us": max(last_idle) if last_idle else None,
+        "term_seen_us": [min(terms), max(terms)] if terms else None,
+        "last_exit_us": end, "busy_worker_us": busy_us, "mean_active": busy_us / end if end else 0,
+        "spills": spills, "bin_us": width, "active_per_bin": [round(c, 1) for c in curve],
+    }
+
+
+def main():
+    out = sys.argv[1]
+    names = sys.argv[2:] or ["T1", "T1L", "T1XL:7"]
+    H.init(0)
+    with open(out, "a") as f:
+        for name in names:
+            tree, _, split = name.partition(":")
+            args, nodes = TREES[tree]
+            shards = [(s, 8, int(split)) for s in range(8)] if split else [(0, 1, 0)]
+            tot = 0
+            for shard, nsh, sp in shards:
+                H.uts(args, shard, nsh, sp)  # warm (tables, code)
+                r = H.uts(args, shard, nsh, sp)
+                tot += r["nodes"]
+                s = summarise(H.last_timeline(), r["kernel_ms"])
+                s.update({"tree": tree, "shard": shard, "nshards": nsh, "split": sp, "nodes": r["nodes"],
+                          "env": {k: v for k, v in os.environ.items() if k.startswith("HCLIB_HIP_")}})
+                f.write(json.dumps(s) + "\n")
+                f.flush()
+                print(tree, shard, f"{r['kernel_ms']:.3f} ms", "start", round(s["start_spread_us"], 1),
+                      "held", s["first_work_us"], "done", round(s["last_item_done_us"], 1), "term",
+                      s["term_seen_us"], "exit", round(s["last_exit_us"], 1), "mean_active",
+                      round(s["mean_active"], 1), flush=True)
+            assert tot == nodes, (name, tot, nodes)
+
+
+if __name__ == "__main__":
+    main()

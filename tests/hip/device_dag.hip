@@ -122,6 +122,44 @@ struct DoublePutKind {
     __device__ static void run(const Ctx &, hx::DagWave &w, uint32_t t, const uint32_t *) { hx::dag_put(w, 0, t); }
 };
 
+// ----------------------------------- workgroup tasks with reserved slots
+// A tagged, reserving Kind (hx_dag.h kTagged / kReserve) on run_dag_group:
+// outputs are tagged words {1 << 32 | value} its readers poll, the put is
+// split around the body and takes one ready slot per waiter entry. Task 0's
+// promise has `fan` (> 64) waiters: the reserved put's long-list form.
+struct ReserveKind {
+    static constexpr int kPutN = 1;
+    static constexpr bool kSc1Payload = true;
+    static constexpr bool kTagged = true;
+    static constexpr bool kReserve = true;
+    struct Ctx {
+        u64 *out;     // tagged output word per task
+        int dbl;      // 1: task 1 also puts promise 0 (a second put)
+        unsigned *bad;
+    };
+    __device__ static u64 wait_tag(const u64 *p) {
+        u64 v = 0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (((v = hx::ld_agent(p)) >> 32) == 0 && __builtin_amdgcn_s_memrealtime() - t0 < 100000000ull)
+            __builtin_amdgcn_s_sleep(1);
+        return v;
+    }
+    __device__ static bool run_group(const Ctx &c, uint32_t t, const uint32_t *pl, int wave) {
+        if (wave != 0) return true;
+        // payload: {value source task or ~0}
+        u64 v = 12345;
+        if (pl[0] != 0xffffffffu) {
+            const u64 in = wait_tag(&c.out[pl[0]]);
+            if ((in >> 32) == 0 && hx::lane_id() == 0) atomicAdd(c.bad, 1u);
+            v = (u64)(uint32_t)in + 7ull * t;
+        }
+        if (hx::lane_id() == 0) hx::st_agent(&c.out[t], (1ull << 32) | (uint32_t)v);
+        return true;
+    }
+    __device__ static void promises(const Ctx &c, uint32_t t, uint32_t (&p)[1]) { p[0] = (c.dbl && t == 1) ? 0 : t; }
+    __device__ static void datums(const Ctx &, uint32_t t, unsigned long long (&d)[1]) { d[0] = t; }
+};
+
 static void report(const char *what, const hclib_hip_dag_stats_t &st) {
     printf("%-10s %8llu tasks %8llu puts %8llu releases  %8.3f ms  %.1f M tasks/s\n", what,
            (unsigned long long)st.tasks, (unsigned long long)st.puts, (unsigned long long)st.releases, st.kernel_ms,
@@ -230,6 +268,55 @@ int main() {
         for (uint32_t t = 1; t < N; ++t) CHECK(g.datum(t) == 12345ull + 7ull * t, "fan-out: promise %u", t);
         CHECK(st.releases == N - 1, "fan-out releases %llu", (unsigned long long)st.releases);
         report("fan-out", st);
+    }
+    {  // workgroup tasks, reserved ready slots, a 200-waiter promise and a chain
+        const uint32_t fan = 200, chain = 300, N = 1 + fan + chain;
+        hclib::hip::dag g(1);
+        for (uint32_t t = 0; t < N; ++t) g.promise();
+        const uint32_t root = 0xffffffffu;
+        g.async_await(&root, nullptr, 0);
+        for (uint32_t t = 1; t <= fan; ++t) {
+            const uint32_t src = 0;
+            g.async_await(&src, {0u});
+        }
+        for (uint32_t t = fan + 1; t < N; ++t) {  // each awaits the previous task (one waiter per promise)
+            const uint32_t src = t - 1;
+            g.async_await(&src, {t - 1});
+        }
+        u64 *out = nullptr;
+        unsigned *bad = nullptr;
+        CHECK(hipMalloc((void **)&out, N * 8) == hipSuccess && hipMalloc((void **)&bad, 4) == hipSuccess, "hipMalloc");
+        CHECK(hipMemset(out, 0, N * 8) == hipSuccess && hipMemset(bad, 0, 4) == hipSuccess, "memset");
+        hclib_hip_dag_stats_t st;
+        for (int waves = 1; waves <= 2; ++waves) {
+            CHECK(hipMemset(out, 0, N * 8) == hipSuccess, "memset");
+            int rc = hclib::hip::run_dag_groups<ReserveKind>(ReserveKind::Ctx{out, 0, bad}, g, &st, 1, waves);
+            CHECK(rc == HCLIB_HIP_OK, "reserved: %s", hclib_hip_last_error());
+            std::vector<u64> got(N);
+            unsigned nbad = 0;
+            CHECK(hipMemcpy(got.data(), out, N * 8, hipMemcpyDeviceToHost) == hipSuccess, "copy back");
+            CHECK(hipMemcpy(&nbad, bad, 4, hipMemcpyDeviceToHost) == hipSuccess, "copy back");
+            CHECK(nbad == 0, "reserved: %u untagged inputs", nbad);
+            u64 want = 12345;
+            for (uint32_t t = 0; t < N; ++t) {
+                u64 w = t == 0 ? 12345 : (t <= fan ? 12345 + 7ull * t : want + 7ull * t);
+                if (t == 0 || t > fan) want = (uint32_t)w;
+                CHECK(got[t] == ((1ull << 32) | (uint32_t)w), "reserved: task %u got %llx", t, (unsigned long long)got[t]);
+                CHECK(g.satisfied(t) && g.datum(t) == t, "reserved: promise %u", t);
+            }
+            CHECK(st.tasks == N && st.puts == N && st.releases == N - 1, "reserved stats %llu %llu %llu",
+                  (unsigned long long)st.tasks, (unsigned long long)st.puts, (unsigned long long)st.releases);
+            report(waves == 1 ? "reserved1" : "reserved2", st);
+        }
+        // a second put on the 200-waiter promise: found (slots past the list
+        // or a satisfied count of 2), promptly, without a hang
+        CHECK(hipMemset(out, 0, N * 8) == hipSuccess, "memset");
+        int rc = hclib::hip::run_dag_groups<ReserveKind>(ReserveKind::Ctx{out, 1, bad}, g, &st, 1, 1, 2000);
+        CHECK(rc == HCLIB_HIP_EDEVICE && strstr(hclib_hip_last_error(), "single assignment"),
+              "reserved double put: rc %d (%s)", rc, hclib_hip_last_error());
+        printf("reserved double put -> %s (%.3f ms)\n", hclib_hip_last_error(), st.kernel_ms);
+        (void)hipFree(out);
+        (void)hipFree(bad);
     }
     {  // a second put on one promise
         hclib::hip::dag g(0);

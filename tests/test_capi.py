@@ -33,7 +33,8 @@ def _run(exe, *args, timeout=300, env=None):
                           timeout=timeout, env=e)
 
 
-@pytest.mark.parametrize("name", ["promise_chain", "fib_gpu", "forasync1DCh_gpu", "uts_gpu", "mem_locale"])
+@pytest.mark.parametrize("name", ["promise_chain", "fib_gpu", "forasync1DCh_gpu", "uts_gpu", "mem_locale",
+                                  "locale_idle"])
 def test_c_programs_compile_against_hclib_h(name):
     assert os.path.exists(_build(name))
 
@@ -42,6 +43,16 @@ def test_host_promise_semantics():
     r = _run(_build("promise_chain"))
     assert r.returncode == 0, r.stderr
     assert "Check results: OK" in r.stdout
+
+
+def test_locale_tasks_idle_functions_and_harness_timer():
+    """locale_num_tasks / locale_register_idle_task / locale_run_idle_tasks
+    (inc/hclib-locality-graph.h:102-105) and hclib_user_harness_timer
+    (inc/hclib-rt.h:153): link, call, reference semantics."""
+    r = _run(_build("locale_idle"), env={"HCLIB_STATS": "1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Check results: OK" in r.stdout
+    assert "User harness timer: 1.250000 s" in r.stdout
 
 
 def test_host_locale_memory_operations():

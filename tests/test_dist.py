@@ -199,3 +199,57 @@ def test_bench_work_sharing_leg_reports_setup_failure():
     for r, out in res:
         assert "error" in out and "static" not in out and "shared" not in out
         assert out["workload"].startswith("test/uts T1L")
+
+
+# ------------------------------------------------------ stalled-leg guard
+# bench.py runs its N > 1 legs under dist.LegGuard: here rank 1 stalls in the
+# first leg (it never enters the collective rank 0 waits in), so rank 0's leg
+# times out; both ranks then skip the second leg (the stall is flagged in the
+# rendezvous store), rank 0 still produces its line within the bound, and
+# every rank leaves with os._exit as bench.py does.
+def _stall_worker(rank, world, port, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HCLIB_DIST_TIMEOUT_S": "60"})
+    import threading
+    import time
+
+    import torch
+    import torch.distributed as tdist
+
+    from hclib_amd import dist
+
+    r, w, _ = dist.init_from_env("gloo")
+    legs = dist.LegGuard(w, 4.0)
+
+    def leg_a():
+        if r == 1:
+            threading.Event().wait()  # stalls forever
+        t = torch.ones(1)
+        tdist.all_reduce(t)  # rank 0 waits here for rank 1
+        return {"sum": float(t[0])}
+
+    t0 = time.monotonic()
+    a = legs.run("a", leg_a)
+    b = legs.run("b", lambda: {"ok": True})
+    q.put((r, a, b, legs.stalled, time.monotonic() - t0))
+    q.close()
+    q.join_thread()  # the feeder thread flushes before the hard exit
+    os._exit(0)
+
+
+def test_stalled_leg_is_reported_and_the_line_still_prints():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stall_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r, a, b, stalled, el in res:
+        assert "timeout" in a["failed"], (r, a)
+        assert b["failed"].startswith("skipped"), (r, b)
+        assert stalled
+        assert el < 30, el  # the guard's bound (4 s per leg), not the collective's 60 s
