@@ -11,6 +11,7 @@
 // the GPU analogue of help_finish's work-shift (no stacks, no fibers). This
 // also is the DDT form (fib.c:113-141): the scope word is the promise pair
 // subres[0..1] and the last put releases fib_ddt_res.
+#include <stdio.h>
 #include <string.h>
 
 #include "hx_module.h"
@@ -20,8 +21,13 @@ namespace hx {
 
 struct FibCtx {
     int n;
+    int local;  // scopes in the wave's LDS while they stay inside it (hx_finish.h LocalScopes)
     FinishArena fin;
 };
+
+// the wave's LDS finish scopes (file scope: every access is a ds_* op)
+constexpr int kFibLocalScopes = 512;
+__shared__ LocalScopes<kFibLocalScopes> s_fib_scopes;
 
 struct FibKind {
     // template = {n + 1 of the parent call, the parent's scope}; child k is
@@ -33,12 +39,10 @@ struct FibKind {
     using Ctx = FibCtx;
     struct Acc {
         unsigned long long tasks = 0, joins = 0;
-        __device__ void flush(SchedGlobals *g) {
-            unsigned long long t = wave_sum(tasks), j = wave_sum(joins);
-            if (lane_id() == 0) {
-                add_agent(&g->counters[0], t);
-                add_agent(&g->counters[1], j);
-            }
+        // the wave's totals go into its exit record (hx_sched.h Kind concept)
+        __device__ void totals(unsigned long long (&c)[8], unsigned long long (&)[4]) {
+            c[0] = wave_sum(tasks);
+            c[1] = wave_sum(joins);
         }
     };
 
@@ -55,15 +59,24 @@ struct FibKind {
         const bool spawn = n >= 2;
         // FINISH { async fib(n-1); async fib(n-2); }  (one bump allocation
         // per wave for every lane that opens a scope)
-        const uint32_t j = finish_open(c.fin, spawn, t[1], 2, 0, err);
+        const uint32_t j = c.local ? finish_open_local(c.fin, s_fib_scopes, spawn, t[1], 2, 0, err)
+                                   : finish_open(c.fin, spawn, t[1], 2, 0, err);
         if (!spawn) {  // a leaf returns n: check out, continuations inline
-            acc.joins += finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
+            acc.joins += c.local ? finish_check_out_local(c.fin, s_fib_scopes, t[1], (unsigned long long)n, PassSum())
+                                 : finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
             return 0;
         }
         if (j == kScopeRoot) return 0;  // arena error (reported)
         child[0] = (uint32_t)n;  // children fib(n-1), fib(n-2)
         child[1] = j;
         return 2;
+    }
+
+    // an item leaving the wave names an HBM scope (its LDS scope promoted)
+    __device__ static void export_item(const Ctx &c, uint32_t *w, bool valid, uint32_t *err) {
+        if (!c.local) return;
+        const uint32_t s = finish_promote(c.fin, s_fib_scopes, valid ? w[1] : kScopeRoot, err);
+        if (valid) w[1] = s;
     }
 };
 
@@ -72,6 +85,7 @@ constexpr int kFibCap = 1024;  // ring items per wave (16 KiB of LDS)
 __global__ __launch_bounds__(64) void k_fib(FibCtx ctx, PoolView pool, SchedGlobals *g,
                                             SchedConfig cfg) {
     __shared__ WaveStack<FibKind, kFibCap> st;
+    if (ctx.local) s_fib_scopes.init();
     run_worker<FibKind, kFibCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
 }
 
@@ -103,6 +117,7 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     HX_HIP(hipMalloc(&dmem, jb + 512));
     FibCtx ctx;
     ctx.n = n;
+    ctx.local = env_int("HCLIB_HIP_FIB_LOCAL", 0);  // LDS scopes: measured slower so far (profiles/r04/fib_stamps.log)
     ctx.fin.scopes = (FinishScope *)dmem;
     ctx.fin.next = (uint32_t *)((char *)dmem + ((jb + 255) & ~(size_t)255));
     ctx.fin.cap = (uint32_t)(scopes + 1);
@@ -126,7 +141,7 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_FIB_HUNGER", 8);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 1);
-    HX_TRY(reset_sched(pool, 1));
+    HX_TRY(reset_sched(pool, 1, false, (uint32_t)grid));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     hipLaunchKernelGGL(k_fib, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
     HX_HIP(hipGetLastError());
@@ -135,6 +150,11 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     int rc = finish_sched(&gl, "hclib_hip_fib");
     unsigned long long v = 0;
     if (rc == HCLIB_HIP_OK) rc = hip_check(hipMemcpy(&v, ctx.fin.root_value, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc == HCLIB_HIP_OK && env_int("HCLIB_HIP_FIB_DEBUG", 0)) {
+        uint32_t used = 0;  // scopes that lived in HBM (opened there or promoted from LDS)
+        if (hipMemcpy(&used, ctx.fin.next, 4, hipMemcpyDeviceToHost) == hipSuccess)
+            fprintf(stderr, "fib(%d): %u of %llu scopes in HBM (local %d)\n", n, used, scopes - 1, ctx.local);
+    }
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
     (void)hipFree(dmem);

@@ -31,6 +31,9 @@ struct Module {
     WaveStat *wave_stats = nullptr;
     uint32_t wave_stats_cap = 0;
     std::vector<WaveStat> last_waves;  // the last launch's, copied back by finish_sched
+    // per-worker exit records (hx_sched.h kWaveCtrWords), summed by finish_sched
+    unsigned long long *wave_ctr = nullptr;
+    uint32_t rec_workers = 0;  // records the running launch writes
     // cross-GPU work sharing (hclib_hip_global_attach): the shared region's
     // view for sharded launches, hdr null while detached
     GlobalView gview = {nullptr, nullptr, nullptr, 0, 0};
@@ -51,7 +54,9 @@ int upload_async(void *dst, const void *src, size_t bytes, hipStream_t stream);
 // Carve a PoolView for `words` u32 per entry out of the arena (grows it).
 int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolView *out);
 // Reset the deques and the globals on the module stream before a launch.
-int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global = false);
+// `workers`: the launch's worker count (its exit records are summed by
+// finish_sched); 0 = exit counts as atomics only
+int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global = false, uint32_t workers = 0);
 // Read back globals and translate the device error word.
 int finish_sched(SchedGlobals *host_copy, const char *who);
 

@@ -136,7 +136,7 @@ int upload_async(void *dst, const void *src, size_t bytes, hipStream_t st) {
     return HCLIB_HIP_OK;
 }
 
-int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global) {
+int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global, uint32_t workers) {
     Module &m = g_mod;
     HX_HIP(hipMemsetAsync(pool.hdr, 0, sizeof(QueueHdr) * pool.nq, m.stream));
     const uint32_t total = pool.nq * pool.cap;
@@ -148,6 +148,9 @@ int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global) {
     init.outstanding = outstanding_init;
     init.wave_stats = m.wave_stats;
     init.wave_stats_cap = m.wave_stats_cap;
+    m.rec_workers = workers < m.wave_stats_cap ? workers : m.wave_stats_cap;
+    init.wave_ctr = m.rec_workers ? m.wave_ctr : nullptr;
+    init.wave_ctr_cap = m.rec_workers;
     if (global) init.gview = m.gview;
     // diagnostic timelines: only a HX_TIMELINE build writes them
     const int tl_cap = env_int("HCLIB_HIP_TIMELINE", 0);
@@ -189,7 +192,24 @@ int finish_sched(SchedGlobals *host_copy, const char *who) {
     HX_HIP(hipMemcpyAsync(host_copy, m.globals, sizeof(SchedGlobals), hipMemcpyDeviceToHost,
                           m.stream));
     const uint32_t nw_cap = m.wave_stats_cap;
+    // the workers' exit records (every worker of the grid writes its own)
+    static std::vector<unsigned long long> rec;
+    const uint32_t nrec = m.rec_workers;
+    m.rec_workers = 0;
+    if (nrec) {
+        rec.resize((size_t)nrec * kWaveCtrWords);
+        HX_HIP(hipMemcpyAsync(rec.data(), m.wave_ctr, rec.size() * 8, hipMemcpyDeviceToHost, m.stream));
+    }
     HX_HIP(hipStreamSynchronize(m.stream));
+    for (uint32_t w = 0; w < nrec; ++w) {
+        const unsigned long long *r = &rec[(size_t)w * kWaveCtrWords];
+        for (int i = 0; i < 16; ++i)
+            if (i >= 8 || i < 4) host_copy->counters[i] += r[i];
+        for (int i = 4; i < 8; ++i) host_copy->counters[i] += r[24 + i - 4];
+        for (int i = 0; i < 4; ++i)
+            if (r[16 + i] > host_copy->maxes[i]) host_copy->maxes[i] = r[16 + i];
+        for (int i = 0; i < 3; ++i) host_copy->narrow[i] += r[20 + i];
+    }
     memcpy(m.last_counters, host_copy->counters, sizeof(m.last_counters));
     memcpy(m.last_narrow, host_copy->narrow, sizeof(m.last_narrow));
     // every wave of the grid leaves exactly once: counters[kCtrWaves] records
@@ -251,6 +271,7 @@ int hclib_hip_init(int device) {
     HX_HIP(hipMalloc((void **)&m.globals, sizeof(SchedGlobals)));
     m.wave_stats_cap = (uint32_t)m.num_cus * 32;  // 32 waves per CU at most
     HX_HIP(hipMalloc((void **)&m.wave_stats, sizeof(WaveStat) * m.wave_stats_cap));
+    HX_HIP(hipMalloc((void **)&m.wave_ctr, 8ull * kWaveCtrWords * m.wave_stats_cap));
     m.inited = true;
     return HCLIB_HIP_OK;
 }
@@ -262,6 +283,7 @@ void hclib_hip_finalize(void) {
     if (m.pool_mem) (void)hipFree(m.pool_mem);
     (void)hipFree(m.globals);
     (void)hipFree(m.wave_stats);
+    (void)hipFree(m.wave_ctr);
     if (m.timeline) (void)hipFree(m.timeline);
     (void)hipEventDestroy(m.ev0);
     (void)hipEventDestroy(m.ev1);
@@ -309,7 +331,7 @@ int hclib_hip_sched_begin(uint32_t entry_words, uint32_t chunk, int waves_per_cu
     PoolView pool;
     HX_TRY(make_pool((uint32_t)env_int("HCLIB_HIP_DEQUES", 64), (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
                      chunk, entry_words, &pool));
-    HX_TRY(reset_sched(pool, 1));
+    HX_TRY(reset_sched(pool, 1, false, (uint32_t)(m.num_cus * waves_per_cu)));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     out->hdr = pool.hdr;
     out->seq = pool.seq;

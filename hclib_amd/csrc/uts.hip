@@ -185,15 +185,11 @@ struct UtsKind {
         uint32_t trace_seen = 0;  // FEAT 2: the deepest depth this wave has stamped
         uint32_t mode = 0;        // FEAT 2: 1 while the scheduler runs the narrow loop (hx_sched.h)
         uint32_t wid = 0;         // FEAT 2: this worker's id (hx_sched.h acc_set_wid)
-        __device__ void flush(SchedGlobals *g) {
-            unsigned long long n = wave_sum((unsigned long long)nodes),
-                               l = wave_sum((unsigned long long)leaves);
-            uint32_t m = wave_max(maxd);
-            if (lane_id() == 0) {
-                add_agent(&g->counters[0], n);
-                add_agent(&g->counters[1], l);
-                __hip_atomic_fetch_max(&g->maxes[0], (unsigned long long)m, __ATOMIC_RELAXED, HX_AGENT);
-            }
+        // the wave's totals go into its exit record (hx_sched.h Kind concept)
+        __device__ void totals(unsigned long long (&c)[8], unsigned long long (&m)[4]) {
+            c[0] = wave_sum((unsigned long long)nodes);
+            c[1] = wave_sum((unsigned long long)leaves);
+            m[0] = (unsigned long long)wave_max(maxd);
         }
     };
 
@@ -758,9 +754,10 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // whose ring fits two batches' pushes: the fixed-shape GEO trees on
     // 512-item rings)
     cfg.dual = (uint32_t)env_int("HCLIB_HIP_UTS_DUAL", 1);
+    cfg.spill_lo_hungry = (uint32_t)env_int("HCLIB_HIP_SPILL_LO_HUNGRY", 0);
     // sharded launches of a rank attached to a global region share work
     const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
-    HX_TRY(reset_sched(pool, 1, global));
+    HX_TRY(reset_sched(pool, 1, global, (uint32_t)grid));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     const bool feat = nshards > 1 || max_levels > 0;
     if (bin) ctx.bin_thr = (uint32_t)T.rules[1].y;

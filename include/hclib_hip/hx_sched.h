@@ -141,7 +141,19 @@ struct alignas(256) SchedGlobals {
     // worker `timeline_cap` events of lane 0 (see Timeline), or null
     unsigned long long *timeline;
     uint32_t timeline_cap;
+    // per-worker exit records (kWaveCtrWords u64 each, plain stores; the
+    // host sums them into counters / maxes / narrow, finish_sched), or null:
+    // then the exit counts are agent atomics on the lines above. Thousands
+    // of workers adding ~15 counts each to two lines serialised 100-250 us
+    // of every launch's exit (worker timelines, profiles/r04)
+    unsigned long long *wave_ctr;
+    uint32_t wave_ctr_cap;
 };
+// a worker's exit record: [0..7] the kind's counters, [8..15] the
+// scheduler's counters (SchedGlobals::counters [8..15]; [4..7] of the
+// diagnostic stamps go to [24..27]), [16..19] the kind's maxima, [20..22]
+// the narrow-loop counts
+constexpr int kWaveCtrWords = 32;
 
 // Diagnostic build (-DHX_TIMELINE=1, `python -m hclib_amd.build --variant
 // timeline`): every worker logs its transitions — start, busy (work taken),
@@ -233,6 +245,8 @@ struct SchedConfig {
                          // (PendingChunk) instead of behind a store round trip
     uint32_t dual = 1;   // kinds with process2 (KindDual): a wave holding more than 64
                          // items runs TWO per lane per batch, their bodies interleaved
+    uint32_t spill_lo_hungry = 0;  // spill_lo while more than 1/8 of the waves are hungry
+                                   // (ramp-up, the tail of a search); 0: spill_lo always
 };
 
 // Kind concept:
@@ -241,6 +255,10 @@ struct SchedConfig {
 //                                     // payload {template, k, kend}
 //   struct Ctx;                       // per-launch read-only parameters
 //   struct Acc { ...; __device__ void flush(SchedGlobals*); };  // per-lane stats
+//        (optional, in place of flush: __device__ void totals(unsigned long long
+//        (&c)[8], unsigned long long (&m)[4]) — the wave's sums / maxima,
+//        wave-uniform, which the scheduler stores in the worker's exit record
+//        instead of adding them to SchedGlobals::counters / maxes atomically)
 //   __device__ static int process(const Ctx&, Acc&, const uint32_t *tmpl, uint32_t k,
 //                                 uint32_t *child_tmpl, uint32_t *err);
 //        run child k of `tmpl`; return the number of children of the new
@@ -422,6 +440,21 @@ __device__ __forceinline__ void publish_pending(const PoolView &pool, SchedGloba
     pc.live = false;
 }
 
+// Optional Kind hook: static void export_item(const Ctx&, uint32_t *w, bool valid, uint32_t *err)
+// — called by the whole wave for the items it is about to hand to another
+// wave (a chunk, an inbox, the global ring; `w` = {template, k, kend},
+// `valid` = the lane packs an item). A Kind whose templates name wave-local
+// state (fib's LDS finish scopes, hx_finish.h LocalScopes) rewrites them to
+// names every wave can use.
+template <class K, class = void>
+struct kind_has_export : std::false_type {};
+template <class K>
+struct kind_has_export<K, decltype((void)&K::export_item)> : std::true_type {};
+template <class Kind>
+__device__ __forceinline__ void kind_export(const typename Kind::Ctx &ctx, uint32_t *w, bool valid, uint32_t *err) {
+    if constexpr (kind_has_export<Kind>::value) Kind::export_item(ctx, w, valid, err);
+}
+
 // Try to publish `n` entries (ring positions bot..bot+n-1) as one chunk into
 // deque q. Called by the whole wave; returns true if the chunk is placed.
 // `occ`: the deque occupancy this wave saw at its last enqueue. While that
@@ -431,8 +464,9 @@ __device__ __forceinline__ void publish_pending(const PoolView &pool, SchedGloba
 // consumer that cannot come. With `pc`, the publish is deferred (see
 // PendingChunk); the caller must publish a live one before the next enqueue.
 template <class Kind, int CAP>
-__device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q, WaveStack<Kind, CAP> &st,
-                              uint32_t bot, uint32_t n, uint32_t &occ, PendingChunk *pc, bool relief = false) {
+__device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &pool, SchedGlobals *g, uint32_t q,
+                              WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n, uint32_t &occ, PendingChunk *pc,
+                              bool relief = false) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     QueueHdr *h = &pool.hdr[q];
@@ -477,15 +511,19 @@ __device__ bool enqueue_chunk(const PoolView &pool, SchedGlobals *g, uint32_t q,
     }
     // lane i packs item bot+i as {template, k, kend} (n <= 64)
     uint32_t *dst = pool.data + (size_t)slot * pool.chunk * W;
-    if ((uint32_t)lane < n) {
-        const uint32_t p = bot + (uint32_t)lane;
-        const uint2 dd = st.d[p & (CAP - 1)];
+    {
+        const bool valid = (uint32_t)lane < n;
         uint32_t w[W];
+        const uint32_t p = bot + (valid ? (uint32_t)lane : 0u);
+        const uint2 dd = st.d[p & (CAP - 1)];
         load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & (CAP - 1), w);
         w[W - 2] = dd.x;
         w[W - 1] = dd.y & (kMaxChildren - 1);
+        kind_export<Kind>(ctx, w, valid, &g->err);
+        if (valid) {
 #pragma unroll
-        for (int i = 0; i < W; ++i) st_agent(&dst[(uint32_t)lane * W + i], w[i]);
+            for (int i = 0; i < W; ++i) st_agent(&dst[(uint32_t)lane * W + i], w[i]);
+        }
     }
     if (lane == 0) st_agent(slot_ctl(pool, slot) + 1, n);
     if (pc) {
@@ -603,6 +641,7 @@ __device__ bool global_enqueue(const typename Kind::Ctx &ctx, const GlobalView &
         }
     }
     if (!lane0((uint32_t)ok)) return false;
+    kind_export<Kind>(ctx, w, (uint32_t)lane < n, err);
     pos = lane0(pos);
     const uint32_t slot = pos & (gv.cap - 1);
     uint32_t *ctl = gv.ctl + 2u * slot;
@@ -695,6 +734,13 @@ __device__ uint32_t global_dequeue(const GlobalView &gv, uint32_t words_per_chun
     }
     vm_drain();
     return n;
+}
+
+// the give-away threshold: spill_lo, or spill_lo_hungry while more than an
+// eighth of the waves are hungry (a ramp-up, the tail of a search: work then
+// is worth more on an idle wave than deeper in this one's ring)
+__device__ __forceinline__ uint32_t spill_lo_now(const SchedConfig &cfg, uint32_t hungry) {
+    return (cfg.spill_lo_hungry && hungry * 8u > cfg.nwaves) ? cfg.spill_lo_hungry : cfg.spill_lo;
 }
 
 __device__ __forceinline__ uint32_t xorshift(uint32_t &s) {
@@ -875,6 +921,11 @@ __device__ __forceinline__ void acc_set_mode(A &a, uint32_t m) {
 }
 // ... and a `wid` field the running worker's id (diagnostic traces)
 template <class A, class = void>
+struct acc_has_totals : std::false_type {};
+template <class A>
+struct acc_has_totals<A, decltype((void)&A::totals)> : std::true_type {};
+
+template <class A, class = void>
 struct acc_has_wid : std::false_type {};
 template <class A>
 struct acc_has_wid<A, decltype((void)A::wid)> : std::true_type {};
@@ -972,7 +1023,8 @@ struct Inbox {
 };
 
 template <class Kind, int CAP>
-__device__ bool inbox_put(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n, SchedGlobals *g) {
+__device__ bool inbox_put(const typename Kind::Ctx &ctx, Inbox<Kind> &ib, WaveStack<Kind, CAP> &st, uint32_t bot,
+                          uint32_t n, SchedGlobals *g) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     uint32_t ok = 0;
@@ -984,15 +1036,19 @@ __device__ bool inbox_put(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st, uint32_t bo
                  : 0u;
     }
     if (!lane0(ok)) return false;
-    if ((uint32_t)lane < n) {
-        const uint32_t p = bot + (uint32_t)lane;
+    {
+        const bool valid = (uint32_t)lane < n;
+        const uint32_t p = bot + (valid ? (uint32_t)lane : 0u);
         const uint2 dd = st.d[p & (CAP - 1)];
         uint32_t w[W];
         load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & (CAP - 1), w);
         w[W - 2] = dd.x;
         w[W - 1] = dd.y & (kMaxChildren - 1);
+        kind_export<Kind>(ctx, w, valid, &g->err);
+        if (valid) {
 #pragma unroll
-        for (int i = 0; i < W; ++i) ib.w[(uint32_t)lane * W + i] = w[i];
+            for (int i = 0; i < W; ++i) ib.w[(uint32_t)lane * W + i] = w[i];
+        }
     }
     asm volatile("" ::: "memory");
     if (lane == 0) {
@@ -1347,10 +1403,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 if (n > pool.chunk) n = pool.chunk;
                 bool ok = false;
                 for (uint32_t a = 0; a < pool.nq && !ok; ++a)
-                    ok = enqueue_chunk<Kind, CAP>(pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr);
+                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr);
                 // every deque is at its half mark: fill one past it rather than wait
                 for (uint32_t a = 0; a < pool.nq && !ok; ++a)
-                    ok = enqueue_chunk<Kind, CAP>(pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr, true);
+                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr, true);
                 if (!ok) {
                     // every deque is full: other waves are draining them, so wait
                     // (bounded) rather than fail at once
@@ -1494,7 +1550,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         {
             const uint32_t hungry0 = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
             if (cfg.carry && uniform && tout > 0 && tout <= (uint32_t)kWaveSize &&
-                !(hungry0 > 0 && (top - bot) + tout >= cfg.spill_lo)) {
+                !(hungry0 > 0 && (top - bot) + tout >= spill_lo_now(cfg, hungry0))) {
                 carry_permute<TW>(spawn, mu, nch, child, ctmpl, ck);
                 carry = tout;
                 if (HX_STAMPS && cfg.stamps) cyc_push += __builtin_amdgcn_s_memtime() - ts0;
@@ -1549,9 +1605,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         // ---- give the oldest items to hungry waves, or relieve a full ring
         uint32_t sz = top - bot;
         uint32_t hungry = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
-        if (sz > cfg.spill_hi || (hungry > 0 && sz >= cfg.spill_lo)) {
+        const uint32_t lo = spill_lo_now(cfg, hungry);
+        if (sz > cfg.spill_hi || (hungry > 0 && sz >= lo)) {
             const unsigned long long ts = __builtin_amdgcn_s_memtime();
-            while (sz > cfg.spill_hi || (hungry > 0 && sz >= cfg.spill_lo)) {
+            while (sz > cfg.spill_hi || (hungry > 0 && sz >= lo)) {
                 uint32_t n = (sz + 1) / 2;
                 if (n > pool.chunk) n = pool.chunk;
                 if (n == 0 || n == sz) break;
@@ -1563,13 +1620,13 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                         Inbox<Kind> &sib = ib[(wave + a) % (uint32_t)WPG];
                         if (lane0(*(volatile uint32_t *)&sib.idle) == 1u &&
                             lane0(*(volatile uint32_t *)&sib.state) == 0u)
-                            ok = inbox_put<Kind, CAP>(sib, st, bot, n, g);
+                            ok = inbox_put<Kind, CAP>(ctx, sib, st, bot, n, g);
                     }
                 }
                 if (!ok) publish_pending<Kind, CAP>(pool, g, pend);  // one deferred chunk at a time
                 for (uint32_t a = 0; a < qpx && !ok; ++a) {
                     const uint32_t q = xcc * qpx + (home - xcc * qpx + a) % qpx;
-                    ok = enqueue_chunk<Kind, CAP>(pool, g, q, st, bot, n, occ, cfg.defer ? &pend : nullptr);
+                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, q, st, bot, n, occ, cfg.defer ? &pend : nullptr);
                 }
                 if (!ok) break;  // deques full: keep the items (the ring still has room)
                 ++npush;
@@ -1617,7 +1674,19 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         // only reached on an error break: keep the protocol consistent
         wave_goes_idle<GLOBAL>(g, gv, pool);
     }
-    acc.flush(g);
+    const bool rec = g->wave_ctr && gid < g->wave_ctr_cap;
+    unsigned long long kc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, km[4] = {0, 0, 0, 0};
+    if constexpr (acc_has_totals<typename Kind::Acc>::value) {
+        acc.totals(kc, km);
+        if (!rec && lane == 0) {
+            for (int i = 0; i < 8; ++i)
+                if (kc[i]) add_agent(&g->counters[i], kc[i]);
+            for (int i = 0; i < 4; ++i)
+                if (km[i]) __hip_atomic_fetch_max(&g->maxes[i], km[i], __ATOMIC_RELAXED, HX_AGENT);
+        }
+    } else {
+        acc.flush(g);
+    }
     {
         // this wave's record (plain stores: the host reads it after the launch)
         const unsigned long long ex = wave_sum((unsigned long long)n_exec),
@@ -1638,26 +1707,59 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             ((unsigned long long *)&g->wave_stats[gid])[lane] = v;
         }
     }
-    if (lane == 0 && n_narrow_in) {
-        add_agent(&g->narrow[0], (unsigned long long)n_narrow);
-        add_agent(&g->narrow[1], cyc_narrow);
-        add_agent(&g->narrow[2], (unsigned long long)n_narrow_in);
-    }
-    if (lane == 0) {
-        add_agent(&g->counters[kCtrBusyCycles], cyc_busy);
-        if (HX_STAMPS && cfg.stamps) {
-            add_agent(&g->counters[kCtrFormCycles], cyc_form);
-            add_agent(&g->counters[kCtrProcCycles], cyc_proc);
-            add_agent(&g->counters[kCtrPushCycles], cyc_push - cyc_proc);
+    const unsigned long long c_push = (HX_STAMPS && cfg.stamps) ? cyc_push - cyc_proc : 0,
+                             c_form = (HX_STAMPS && cfg.stamps) ? cyc_form : 0,
+                             c_proc = (HX_STAMPS && cfg.stamps) ? cyc_proc : 0;
+    if (rec) {
+        // one store instruction: lane i writes word i of the record
+        unsigned long long v = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (lane == i) v = kc[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (lane == 16 + i) v = km[i];
+        switch (lane) {
+        case 8 + kCtrProcCycles - 8: v = c_proc; break;
+        case 8 + kCtrBusyCycles - 8: v = cyc_busy; break;
+        case 8 + kCtrIdleCycles - 8: v = cyc_idle; break;
+        case 8 + kCtrSpillCycles - 8: v = cyc_spill; break;
+        case 8 + kCtrWaves - 8: v = 1; break;
+        case 8 + kCtrBatches - 8: v = nbatch; break;
+        case 8 + kCtrPushed - 8: v = npush; break;
+        case 8 + kCtrStolen - 8: v = nsteal; break;
+        case 20: v = n_narrow_in ? (unsigned long long)n_narrow : 0; break;
+        case 21: v = n_narrow_in ? cyc_narrow : 0; break;
+        case 22: v = n_narrow_in; break;
+        case 24 + kCtrPushCycles - 4: v = c_push; break;
+        case 24 + kCtrClockTicks - 4: v = t_end - t_begin; break;
+        case 24 + kCtrRealTicks - 4: v = rt_end - rt_begin; break;
+        case 24 + kCtrFormCycles - 4: v = c_form; break;
+        default: break;
         }
-        add_agent(&g->counters[kCtrIdleCycles], cyc_idle);
-        add_agent(&g->counters[kCtrSpillCycles], cyc_spill);
-        add_agent(&g->counters[kCtrWaves], 1ull);
-        add_agent(&g->counters[kCtrBatches], (unsigned long long)nbatch);
-        add_agent(&g->counters[kCtrPushed], (unsigned long long)npush);
-        add_agent(&g->counters[kCtrStolen], (unsigned long long)nsteal);
-        add_agent(&g->counters[kCtrClockTicks], t_end - t_begin);
-        add_agent(&g->counters[kCtrRealTicks], rt_end - rt_begin);
+        if (lane < kWaveCtrWords) g->wave_ctr[(size_t)gid * kWaveCtrWords + lane] = v;
+    } else {
+        if (lane == 0 && n_narrow_in) {
+            add_agent(&g->narrow[0], (unsigned long long)n_narrow);
+            add_agent(&g->narrow[1], cyc_narrow);
+            add_agent(&g->narrow[2], (unsigned long long)n_narrow_in);
+        }
+        if (lane == 0) {
+            add_agent(&g->counters[kCtrBusyCycles], cyc_busy);
+            if (HX_STAMPS && cfg.stamps) {
+                add_agent(&g->counters[kCtrFormCycles], c_form);
+                add_agent(&g->counters[kCtrProcCycles], c_proc);
+                add_agent(&g->counters[kCtrPushCycles], c_push);
+            }
+            add_agent(&g->counters[kCtrIdleCycles], cyc_idle);
+            add_agent(&g->counters[kCtrSpillCycles], cyc_spill);
+            add_agent(&g->counters[kCtrWaves], 1ull);
+            add_agent(&g->counters[kCtrBatches], (unsigned long long)nbatch);
+            add_agent(&g->counters[kCtrPushed], (unsigned long long)npush);
+            add_agent(&g->counters[kCtrStolen], (unsigned long long)nsteal);
+            add_agent(&g->counters[kCtrClockTicks], t_end - t_begin);
+            add_agent(&g->counters[kCtrRealTicks], rt_end - rt_begin);
+        }
     }
     tl.log(kTlEnd, 0);
 }

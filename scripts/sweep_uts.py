@@ -12,6 +12,8 @@ TREES = {"T1": ("-t 1 -a 3 -d 10 -b 4 -r 19", 4130071),
          "T3L": ("-t 0 -b 2000 -q 0.200014 -m 5 -r 7", 111345631),
          "T1XL": ("-t 1 -a 3 -d 15 -b 4 -r 29", 1635119272), "fib30": ("fib", 0),
          "T1L": ("-t 1 -a 3 -d 13 -b 4 -r 29", 102181082)}
+tree_arg, _, split_arg = sys.argv[1].partition(":")  # T1XL:7 = bench's 8-way shards at split 7 (slowest)
+sys.argv[1] = tree_arg
 if sys.argv[1] not in TREES:  # any published tree (tests/golden/uts_goldens.json)
     import json
     pub = json.load(open(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "uts_goldens.json")))
@@ -27,6 +29,14 @@ for combo in itertools.product(*[v for _, v in knobs]):
         if args == "fib":
             v, r = H.fib(30)
             assert v == 832040
+        elif split_arg:
+            worst, tot = 0.0, 0
+            for sh in range(8):
+                r = H.uts(args, sh, 8, int(split_arg))
+                tot += r["nodes"]
+                worst = max(worst, r["kernel_ms"])
+            assert tot == nodes
+            r = {"kernel_ms": worst}
         else:
             r = H.uts(args)
             assert r["nodes"] == nodes

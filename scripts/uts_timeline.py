@@ -65,6 +65,20 @@ def summarise(tl, kernel_ms, bins=100):
             lo, hi = max(a, i * width), min(b, (i + 1) * width)
             if hi > lo:
                 curve[i] += (hi - lo) / width
+    # per worker: termination seen / exit / last busy->idle / the event before termination
+    per = []
+    for w in tl:
+        ev = [(us(t), e, v) for t, e, v in w]
+        tt = [t for t, e, _ in ev if e == 5]
+        te = [t for t, e, _ in ev if e == 6]
+        ti = [t for t, e, _ in ev if e == 3]
+        k = next((i for i, (_, e, _) in enumerate(ev) if e == 5), None)
+        before = ev[k - 1][1:] if k else None
+        per.append([round(tt[0], 2) if tt else None, round(te[0], 2) if te else None,
+                    round(ti[-1], 2) if ti else None, before, len(ev)])
+    term_sorted = sorted(x[0] for x in per if x[0] is not None)
+    tq = lambda f: term_sorted[min(len(term_sorted) - 1, int(f * len(term_sorted)))] if term_sorted else None
+    exit_cost = sorted(x[1] - x[0] for x in per if x[0] is not None and x[1] is not None)
     pct = lambda f: held[min(len(held) - 1, int(f * nw))] if len(held) > f * nw else None
     busy_us = sum(b - a for a, b in intervals)
     return {
@@ -75,6 +89,10 @@ def summarise(tl, kernel_ms, bins=100):
         "term_seen_us": [min(terms), max(terms)] if terms else None,
         "last_exit_us": end, "busy_worker_us": busy_us, "mean_active": busy_us / end if end else 0,
         "spills": spills, "bin_us": width, "active_per_bin": [round(c, 1) for c in curve],
+        "term_quantiles_us": {q: tq(q) for q in (0.0, 0.5, 0.9, 0.99, 1.0)},
+        "exit_cost_us": {q: exit_cost[min(len(exit_cost) - 1, int(q * len(exit_cost)))] for q in (0.5, 0.9, 1.0)}
+        if exit_cost else None,
+        "per_worker": per,
     }
 
 
@@ -84,6 +102,17 @@ def main():
     H.init(0)
     with open(out, "a") as f:
         for name in names:
+            if name == "fib30":
+                H.fib(30)
+                v, st = H.fib(30)
+                assert v == 832040
+                s = summarise(H.last_timeline(), st["kernel_ms"])
+                s.update({"tree": "fib30", "env": {k: v for k, v in os.environ.items() if k.startswith("HCLIB_HIP_")}})
+                f.write(json.dumps(s) + "\n")
+                print("fib30", f"{st['kernel_ms']:.3f} ms", "held", s["first_work_us"], "done",
+                      round(s["last_item_done_us"], 1), "exit", round(s["last_exit_us"], 1), "mean_active",
+                      round(s["mean_active"], 1), flush=True)
+                continue
             tree, _, split = name.partition(":")
             args, nodes = TREES[tree]
             shards = [(s, 8, int(split)) for s in range(8)] if split else [(0, 1, 0)]
@@ -100,7 +129,8 @@ def main():
                 print(tree, shard, f"{r['kernel_ms']:.3f} ms", "start", round(s["start_spread_us"], 1),
                       "held", s["first_work_us"], "done", round(s["last_item_done_us"], 1), "term",
                       s["term_seen_us"], "exit", round(s["last_exit_us"], 1), "mean_active",
-                      round(s["mean_active"], 1), flush=True)
+                      round(s["mean_active"], 1), "term_q", s["term_quantiles_us"], "exit_cost",
+                      s["exit_cost_us"], flush=True)
             assert tot == nodes, (name, tot, nodes)
 
 

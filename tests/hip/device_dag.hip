@@ -297,11 +297,12 @@ int main() {
             CHECK(hipMemcpy(got.data(), out, N * 8, hipMemcpyDeviceToHost) == hipSuccess, "copy back");
             CHECK(hipMemcpy(&nbad, bad, 4, hipMemcpyDeviceToHost) == hipSuccess, "copy back");
             CHECK(nbad == 0, "reserved: %u untagged inputs", nbad);
-            u64 want = 12345;
+            std::vector<uint32_t> want(N);
             for (uint32_t t = 0; t < N; ++t) {
-                u64 w = t == 0 ? 12345 : (t <= fan ? 12345 + 7ull * t : want + 7ull * t);
-                if (t == 0 || t > fan) want = (uint32_t)w;
-                CHECK(got[t] == ((1ull << 32) | (uint32_t)w), "reserved: task %u got %llx", t, (unsigned long long)got[t]);
+                // task t reads task pl[0]'s output: 0 for the fan, t - 1 along the chain
+                want[t] = t == 0 ? 12345u : (uint32_t)(want[t <= fan ? 0 : t - 1] + 7ull * t);
+                CHECK(got[t] == ((1ull << 32) | want[t]), "reserved: task %u got %llx want %x", t,
+                      (unsigned long long)got[t], want[t]);
                 CHECK(g.satisfied(t) && g.datum(t) == t, "reserved: promise %u", t);
             }
             CHECK(st.tasks == N && st.puts == N && st.releases == N - 1, "reserved stats %llu %llu %llu",
