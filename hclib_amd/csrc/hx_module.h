@@ -33,6 +33,9 @@ struct Module {
     std::vector<WaveStat> last_waves;  // the last launch's, copied back by finish_sched
     // per-worker exit records (hx_sched.h kWaveCtrWords), summed by finish_sched
     unsigned long long *wave_ctr = nullptr;
+    // breadth-first seeding arena (two level buffers + control lines)
+    void *seed_mem = nullptr;
+    size_t seed_bytes = 0;
     uint32_t rec_workers = 0;  // records the running launch writes
     // cross-GPU work sharing (hclib_hip_global_attach): the shared region's
     // view for sharded launches, hdr null while detached
@@ -56,7 +59,14 @@ int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolVie
 // Reset the deques and the globals on the module stream before a launch.
 // `workers`: the launch's worker count (its exit records are summed by
 // finish_sched); 0 = exit counts as atomics only
-int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global = false, uint32_t workers = 0);
+// `seed` (optional): breadth-first seeding of the launch (hx_sched.h
+// seed_levels) with this many slots per level before the share-out, entries
+// of `seed_words` u32; outstanding then starts at `workers`
+struct SeedCfg {
+    uint32_t target, max_levels, words, min_levels;
+};
+int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global = false, uint32_t workers = 0,
+                const SeedCfg *seed = nullptr);
 // Read back globals and translate the device error word.
 int finish_sched(SchedGlobals *host_copy, const char *who);
 

@@ -136,7 +136,8 @@ int upload_async(void *dst, const void *src, size_t bytes, hipStream_t st) {
     return HCLIB_HIP_OK;
 }
 
-int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global, uint32_t workers) {
+int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global, uint32_t workers,
+                const SeedCfg *seed) {
     Module &m = g_mod;
     HX_HIP(hipMemsetAsync(pool.hdr, 0, sizeof(QueueHdr) * pool.nq, m.stream));
     const uint32_t total = pool.nq * pool.cap;
@@ -151,6 +152,28 @@ int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global, ui
     m.rec_workers = workers < m.wave_stats_cap ? workers : m.wave_stats_cap;
     init.wave_ctr = m.rec_workers ? m.wave_ctr : nullptr;
     init.wave_ctr_cap = m.rec_workers;
+    if (seed && seed->target && workers) {
+        // level buffers: a level stops growing at `target` slots, the next one
+        // is at most ~100x a node's... in practice b x target: 8 x target + slack
+        const uint32_t cap = 8u * seed->target + 65536u;
+        const size_t ctl = (size_t)kSeedCtlLines * 256;
+        const size_t need = ctl + 2ull * cap * seed->words * 4;
+        if (need > m.seed_bytes) {
+            if (m.seed_mem) (void)hipFree(m.seed_mem);
+            m.seed_mem = nullptr;
+            m.seed_bytes = 0;
+            HX_HIP(hipMalloc(&m.seed_mem, need));
+            m.seed_bytes = need;
+        }
+        HX_HIP(hipMemsetAsync(m.seed_mem, 0, ctl, m.stream));
+        init.seed.ctl = (uint32_t *)m.seed_mem;
+        init.seed.buf = (uint32_t *)((char *)m.seed_mem + ctl);
+        init.seed.cap = cap;
+        init.seed.target = seed->target;
+        init.seed.max_levels = seed->max_levels;
+        init.seed.min_levels = seed->min_levels;
+        init.outstanding = workers;  // every wave holds a unit until it has its share
+    }
     if (global) init.gview = m.gview;
     // diagnostic timelines: only a HX_TIMELINE build writes them
     const int tl_cap = env_int("HCLIB_HIP_TIMELINE", 0);
@@ -284,6 +307,7 @@ void hclib_hip_finalize(void) {
     (void)hipFree(m.globals);
     (void)hipFree(m.wave_stats);
     (void)hipFree(m.wave_ctr);
+    if (m.seed_mem) (void)hipFree(m.seed_mem);
     if (m.timeline) (void)hipFree(m.timeline);
     (void)hipEventDestroy(m.ev0);
     (void)hipEventDestroy(m.ev1);

@@ -715,12 +715,15 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     int wpc_default = 2, ring_default = 512;
     if (!bin) {
         const double est = uts_expected_nodes(*params);
-        wpc_default = est >= 3e7 ? 8 : (geo_fixed ? 2 : 4);
+        // (fixed-shape trees start seeded, below: T1 then runs fastest on 4
+        // waves per CU and 512-item rings, 0.28 vs 0.61 ms unseeded on 2 / 256,
+        // profiles/r04/seed*_t1.log)
+        wpc_default = est >= 3e7 ? 8 : 4;
         // and a small tree runs faster on 256-item rings (one piece per task:
         // the frontier fans out by range splitting) at 2 waves per CU: T1
         // 0.98 -> 0.70 ms; a large one slower (T1XL 52 -> 70 ms),
         // profiles/r02/sweep_t1_ring_waves.log, sweep_t1xl_ring_waves.log, geo_lds_tail.log
-        ring_default = est >= 3e7 ? 512 : 256;
+        ring_default = (est >= 3e7 || geo_fixed) ? 512 : 256;
     }
     const int grid = env_int("HCLIB_HIP_GRID", 0) > 0
                          ? env_int("HCLIB_HIP_GRID", 0)
@@ -736,7 +739,15 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // at one piece per task (T1XL 37.2 ms, T1L 3.77; profiles/r02/
     // pieces_tune.log; 336 at five pieces), 128 on 256-item rings (T1)
     const int ring_used = geo_fixed && !(nshards > 1 || max_levels > 0) ? env_int("HCLIB_HIP_UTS_RING", ring_default) : 512;
-    const int spill_lo_default = bin ? 72 : (geo_fixed && ring_used < 512) ? 128 : 224;
+    // sharded launches of a rank attached to a global region share work
+    const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
+    int spill_lo_default = bin ? 72 : (geo_fixed && ring_used < 512) ? 128 : 224;
+    // seeded fixed-shape trees (below) start with every wave busy, so a wave
+    // keeps more before it feeds others: T1 0.285 -> 0.248 ms at 336, T1L
+    // 2.70 -> 2.38, T1XL's 8-way shards 4.94 -> 4.75 at 448
+    // (profiles/r04/seed5_*.log, seed6_*.log)
+    const bool seeded = geo_fixed && !global && env_int("HCLIB_HIP_UTS_SEED", 1) && ring_used >= 512;
+    if (seeded) spill_lo_default = uts_expected_nodes(*params) >= 3e7 ? 448 : 336;
     cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", spill_lo_default);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
@@ -755,9 +766,25 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // 512-item rings)
     cfg.dual = (uint32_t)env_int("HCLIB_HIP_UTS_DUAL", 1);
     cfg.spill_lo_hungry = (uint32_t)env_int("HCLIB_HIP_SPILL_LO_HUNGRY", 0);
-    // sharded launches of a rank attached to a global region share work
-    const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
-    HX_TRY(reset_sched(pool, 1, global, (uint32_t)grid));
+    cfg.ramp_chunk = (uint32_t)env_int("HCLIB_HIP_RAMP_CHUNK", 0);
+    cfg.spread = (uint32_t)env_int("HCLIB_HIP_SPREAD", 0);
+    // breadth-first seeding (hx_sched.h seed_levels) for fixed-shape GEO
+    // trees: the grid expands the top levels together and shares the level
+    // that reaches HCLIB_HIP_SEED_PER_WAVE slots per wave out evenly, instead
+    // of growing the busy set from one root by hand-offs
+    SeedCfg seed{0, 0, (uint32_t)UtsKind<kUtsBin, 0>::kWords, 0};
+    if (seeded) {
+        // slots per wave: a few for a small tree (one level fewer to expand),
+        // more for a large one (finer shares, less stealing later;
+        // profiles/r04/seed3_*.log, seed4_*.log)
+        const int per_wave = env_int("HCLIB_HIP_SEED_PER_WAVE", uts_expected_nodes(*params) >= 3e7 ? 32 : 4);
+        seed.target = (uint32_t)(grid * per_wave);
+        seed.max_levels = (uint32_t)env_int("HCLIB_HIP_SEED_LEVELS", 20);
+        // a shard's share is only known past its split: level d holds the
+        // slots of depth d + 1, filtered when they run
+        seed.min_levels = nshards > 1 ? (uint32_t)split_depth : 0u;
+    }
+    HX_TRY(reset_sched(pool, 1, global, (uint32_t)grid, seed.target ? &seed : nullptr));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     const bool feat = nshards > 1 || max_levels > 0;
     if (bin) ctx.bin_thr = (uint32_t)T.rules[1].y;

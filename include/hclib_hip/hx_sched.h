@@ -148,7 +148,19 @@ struct alignas(256) SchedGlobals {
     // of every launch's exit (worker timelines, profiles/r04)
     unsigned long long *wave_ctr;
     uint32_t wave_ctr_cap;
+    // breadth-first seeding of the launch (see seed_levels), or buf null
+    struct Seed {
+        uint32_t *buf;         // two level buffers of `cap` entries, kWords u32 each
+        uint32_t *ctl;         // kSeedCtlLines lines of 64 words (see seed_levels)
+        uint32_t cap;          // entries per level buffer
+        uint32_t target;       // distribute once a level holds at least this many entries
+        uint32_t max_levels;   // ... or after this many levels
+        uint32_t min_levels;   // ... but not before this many (a sharded search: past its split)
+    } seed;
 };
+constexpr int kSeedMaxLevels = 24;
+constexpr int kSeedGoLines = 64;  // "level d is complete" broadcast lines (a wave polls line gid % 64)
+constexpr int kSeedCtlLines = 2 * kSeedMaxLevels + 2 + kSeedGoLines;
 // a worker's exit record: [0..7] the kind's counters, [8..15] the
 // scheduler's counters (SchedGlobals::counters [8..15]; [4..7] of the
 // diagnostic stamps go to [24..27]), [16..19] the kind's maxima, [20..22]
@@ -172,6 +184,9 @@ enum : uint32_t {
     kTlSpill = 4,  // value: items given away (a chunk or an inbox)
     kTlTerm = 5,   // value: 0 — this worker saw the launch's termination
     kTlEnd = 6,    // value: 0 — after the exit reductions
+    kTlProbe = 7,  // value: probe statistics at exit, (kind << 16) | count / 16 (saturating):
+                   // kind 0 probes, 1 empty deques seen, 2 lost head CASes, 3 publish waits (x1 us)
+    kTlSeed = 8,   // value: the seeding level this worker has just seen complete
 };
 struct Timeline {
     unsigned long long *p;
@@ -242,11 +257,15 @@ struct SchedConfig {
     uint32_t hunger_fast = 0;  // batches between hunger reads while many waves are
                                // hungry (0: (hunger + 3) / 4)
     uint32_t defer = 1;  // a hunger spill's chunk is published after the next batch body
-                         // (PendingChunk) instead of behind a store round trip
+                         // (PendingChunk) instead of behind a store round trip; 2: only
+                         // while at most 1/8 of the waves are hungry
     uint32_t dual = 1;   // kinds with process2 (KindDual): a wave holding more than 64
                          // items runs TWO per lane per batch, their bodies interleaved
     uint32_t spill_lo_hungry = 0;  // spill_lo while more than 1/8 of the waves are hungry
                                    // (ramp-up, the tail of a search); 0: spill_lo always
+    uint32_t spread = 0;           // deques a wave's chunks go to (see the spill loop)
+    uint32_t ramp_chunk = 0;       // items per chunk given away while more than 1/8 of the
+                                   // waves are hungry (more, smaller gifts); 0: pool.chunk
 };
 
 // Kind concept:
@@ -548,29 +567,41 @@ __device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &poo
 // head/tail read, the head CAS, the {seq, cnt} pair, the payload; the slot
 // is handed back with a store nobody waits for.
 // `done` (wave-uniform) receives the header's termination flag.
+// Probe statistics of an idle wave (HX_TIMELINE builds: logged at exit)
+struct ProbeStats {
+    uint32_t probes = 0, empty = 0, lost = 0, wait_us = 0;
+};
+
 template <class Kind, int CAP>
 __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Kind, CAP> &st,
-                                  SchedGlobals *g, uint32_t &done) {
+                                  SchedGlobals *g, uint32_t &done, ProbeStats &ps) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     QueueHdr *h = &pool.hdr[q];
     uint32_t pos = 0, fin = 0;
-    int ok = 0;
+    int ok = 0, nonempty = 0;
     if (lane == 0) {
         // one claim attempt: a ticket below the tail, taken by CAS on the head
         const unsigned long long hd2 = ld_agent((const unsigned long long *)&h->head);
         const uint32_t hd = (uint32_t)hd2, tl = ld_agent(&h->tail);
         fin = (uint32_t)(hd2 >> 32);
-        if ((int)(tl - hd) > 0 && cas_agent(&h->head, hd, hd + 1)) {
+        nonempty = (int)(tl - hd) > 0;
+        if (nonempty && cas_agent(&h->head, hd, hd + 1)) {
             pos = hd;
             ok = 1;
         }
     }
     done = lane0(fin);
+    if (HX_TIMELINE) {
+        ps.probes++;
+        if (!lane0((uint32_t)nonempty)) ps.empty++;
+        else if (!lane0((uint32_t)ok)) ps.lost++;
+    }
     if (!lane0((uint32_t)ok)) return 0;
     pos = lane0(pos);
     const uint32_t slot = q * pool.cap + (pos & (pool.cap - 1));
     uint32_t cnt = 0;
+    uint32_t waited = 0;
     if (lane == 0) {
         // the producer holds this ticket and is publishing it (bounded wait)
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -586,7 +617,9 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        if (HX_TIMELINE) waited = (uint32_t)((__builtin_amdgcn_s_memrealtime() - t0) / 100u);
     }
+    if (HX_TIMELINE) ps.wait_us += lane0(waited);
     handoff_consume();
     // uniform (readfirstlane): the ring bounds derived from it stay in SGPRs,
     // so every scheduler branch and loop of the batch is scalar
@@ -1104,6 +1137,202 @@ __device__ __forceinline__ void wave_goes_idle(SchedGlobals *g, const GlobalView
     }
 }
 
+// Breadth-first seeding (SchedGlobals::seed): a tree grown from one root on
+// thousands of waves spends most of a small search handing work out — every
+// generation of hand-offs (batches to fill a ring, a spill, a probe that
+// finds it) only doubles the waves that hold work (worker timelines,
+// profiles/r04). Instead the whole grid first expands the top of the tree
+// level by level: level d is a list of child slots {template, k, k + 1} in
+// HBM; the waves split it into 64-slot blocks, run each slot (Kind::process:
+// counting, sharding and all), and append the children of every node as the
+// slots of level d + 1 (one bump per wave). A level ends when every wave
+// that had a block has counted itself done (ctl line 2d + 1) — only the
+// participants touch the counters; everyone polls one line for a few
+// microseconds. Once a level holds at least `target` slots (or after
+// `max_levels`) every wave takes an equal share of it straight into its ring
+// and the work-stealing loop starts with every wave busy. ctl lines: [2d]
+// slots appended to level d, [2d + 1] waves done with level d, [2 L] the
+// root's level written (wave 0). The host sets `outstanding` to the wave
+// count: every wave holds a unit until its share is taken.
+// Pure kinds only (the slots of a block run branch-free, as in a batch).
+template <class Kind, int CAP>
+__device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Acc &acc, SchedGlobals *g,
+                                WaveStack<Kind, CAP> &st, uint32_t gid, uint32_t nw, uint32_t spin_limit_ms,
+                                uint32_t &n_exec, uint32_t &n_spawn, uint32_t &nbatch, Timeline &tl) {
+    static_assert(Kind::kPure, "breadth-first seeding runs slots branch-free");
+    constexpr int TW = Kind::kTmplWords, W = Kind::kWords;
+    static_assert(TW == 6 && W == 8, "seeding moves 32-byte slots {6-word template, k, k + 1}");
+    const int lane = lane_id();
+    const auto &sd = g->seed;
+    uint32_t *ctl = sd.ctl;
+    auto line = [&](int i) { return ctl + 64 * i; };
+    // go[d]: level d + 1 is complete (written by the level's last participant
+    // into every broadcast line; a wave polls its own)
+    uint32_t *go = line(2 * kSeedMaxLevels + 2 + (int)(gid % kSeedGoLines));
+    uint32_t *err = &g->err;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    auto wait_ge = [&](uint32_t *p, uint32_t want) -> bool {
+        uint32_t v = 0;
+        for (uint32_t n = 0;; ++n) {
+            if (lane == 0) v = ld_agent(p);
+            if (lane0(v) >= want) return true;
+            if ((n & 63) == 63) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * spin_limit_ms) {
+                    if (lane == 0) dev_error(err, kErrSpinTimeout);
+                    return false;
+                }
+                uint32_t e = 0;
+                if (lane == 0) e = ld_agent(err);
+                if (lane0(e)) return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+    // one block of 64 slots of level d (src) -> children as slots of level
+    // d + 1 (dst, count line cnt); false on an overflow (error recorded).
+    // Slots are 32 B {template, k, k + 1}, moved as 16-B sc1 accesses; the
+    // block's children are written flat (output o by lane o % 64, so every
+    // store instruction writes consecutive slots), the lane -> node map
+    // through the wave's (still empty) ring in LDS
+    auto run_block = [&](const uint32_t *src, uint32_t E, uint32_t b, uint32_t *dst, uint32_t *cnt) -> bool {
+        const uint32_t e = b * 64 + (uint32_t)lane;
+        const bool valid = e < E;
+        uint4 s0, s1;
+        ld_sc1_x4x2(src + (size_t)(valid ? e : 0u) * W, s0, s1);
+        const uint32_t tmpl[TW] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y};
+        uint32_t child[TW];
+        const int nc = Kind::process(ctx, acc, tmpl, s1.z, child, err, valid);
+        ++nbatch;
+        const uint32_t u = valid && nc > 0 ? (uint32_t)nc : 0u;
+        n_exec += valid ? 1u : 0u;
+        n_spawn += u;
+        const int S = wave_scan_add((int)u);
+        const uint32_t tot = (uint32_t)lane63(S), excl = (uint32_t)S - u;
+        uint32_t base = 0;
+        if (lane == 0 && tot) base = add_agent(cnt, tot);
+        st.t0[lane] = make_uint4(child[0], child[1], child[2], child[3]);
+        st.t1[lane] = make_uint2(child[4], child[5]);
+        st.d[lane] = make_uint2(excl, u);
+        asm volatile("" ::: "memory");
+        base = lane0(base);
+        if (base + tot > sd.cap) {  // the level buffer is sized by the host; never expected
+            if (lane == 0) dev_error(err, kErrStackOverflow);
+            return false;
+        }
+        for (uint32_t o = (uint32_t)lane; __ballot(o < tot); o += 64) {
+            if (o < tot) {
+                // the node of output o: the last lane whose first output is <= o
+                int lo = 0, hi = 63;
+#pragma unroll
+                for (int it = 0; it < 6; ++it) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (st.d[mid].x <= o) lo = mid;
+                    else hi = mid - 1;
+                }
+                const uint32_t j = o - st.d[lo].x;
+                const uint2 t1 = st.t1[lo];
+                uint32_t *q = dst + (size_t)(base + o) * W;
+                st_sc1_x4(q, st.t0[lo]);
+                st_sc1_x4(q + 4, make_uint4(t1.x, t1.y, j, j + 1));
+            }
+        }
+        asm volatile("" ::: "memory");
+        return true;
+    };
+    auto buf = [&](int d) { return sd.buf + (size_t)(d & 1) * sd.cap * W; };
+    auto stop = [&](uint32_t E, int d) {
+        return E == 0 || d >= (int)sd.max_levels || d + 1 >= kSeedMaxLevels ||
+               (E >= sd.target && d >= (int)sd.min_levels);
+    };
+    // wave 0: the root's slots (level 0), and the narrow top levels on its
+    // own (no grid-wide round trips while a level fits a few batches)
+    constexpr uint32_t kSolo = 256;
+    uint32_t E = 0;
+    int d = 0;
+    if (gid == 0) {
+        uint32_t tmpl[TW];
+        const int rn = Kind::roots(ctx, acc, tmpl);
+        E = rn > 0 ? ((uint32_t)rn < sd.cap ? (uint32_t)rn : sd.cap) : 0u;
+        for (uint32_t e = (uint32_t)lane; e < E; e += 64) {
+            uint32_t *q = buf(0) + (size_t)e * W;
+            st_sc1_x4(q, make_uint4(tmpl[0], tmpl[1], tmpl[2], tmpl[3]));
+            st_sc1_x4(q + 4, make_uint4(tmpl[4], tmpl[5], e, e + 1));
+        }
+        vm_drain();
+        while (!stop(E, d) && E <= kSolo) {
+            for (uint32_t b = 0; b * 64 < E; ++b)
+                if (!run_block(buf(d), E, b, buf(d + 1), line(2 * (d + 1)))) break;
+            vm_drain();  // this wave's slot stores land before it reads them back
+            uint32_t e2 = 0;
+            if (lane == 0) e2 = ld_agent(line(2 * (d + 1)));
+            E = lane0(e2);
+            ++d;
+            tl.log(kTlSeed, (uint32_t)d);
+        }
+        if (lane == 0) {
+            st_agent(line(2 * kSeedMaxLevels + 1), (uint32_t)d);
+            st_agent(line(2 * kSeedMaxLevels), E + 1);  // (release: the slots and d are drained above)
+        }
+        vm_drain();
+    }
+    if (!wait_ge(line(2 * kSeedMaxLevels), 1u)) return 0;
+    if (lane == 0) {
+        E = ld_agent(line(2 * kSeedMaxLevels)) - 1u;
+        d = (int)ld_agent(line(2 * kSeedMaxLevels + 1));
+    }
+    E = lane0(E);
+    d = (int)lane0((uint32_t)d);
+    // the wide levels: the grid's waves, 64 slots a block
+    for (; !stop(E, d); ++d) {
+        const uint32_t nblk = (E + 63) / 64;
+        bool ok = true;
+        for (uint32_t b = gid; b < nblk && ok; b += nw) ok = run_block(buf(d), E, b, buf(d + 1), line(2 * (d + 1)));
+        if (!ok) return 0;
+        // participants count themselves done once their slots are drained; the
+        // last one tells every broadcast line (its count makes level d + 1 final)
+        const uint32_t P = nblk < nw ? nblk : nw;
+        if (gid < P) {
+            vm_drain();
+            uint32_t prev = 0;
+            if (lane == 0) prev = __hip_atomic_fetch_add(line(2 * d + 1), 1u, __ATOMIC_RELEASE, HX_AGENT);
+            if (lane0(prev) + 1u == P) {
+                const uint32_t e2 = lane == 0 ? ld_agent(line(2 * (d + 1))) : 0u;
+                const uint32_t e1 = lane0(e2) + 1u;  // (biased: 0 = not yet)
+                // go line i holds, per level, the next level's size + 1 at word d
+                for (uint32_t i = (uint32_t)lane; i < (uint32_t)kSeedGoLines; i += 64)
+                    st_agent(line(2 * kSeedMaxLevels + 2 + (int)i) + d, e1);
+            }
+        }
+        if (!wait_ge(go + d, 1u)) return 0;
+        uint32_t e2 = 0;
+        if (lane == 0) e2 = ld_agent(go + d);
+        E = lane0(e2) - 1u;
+        tl.log(kTlSeed, (uint32_t)d + 1u);
+    }
+    // this wave's share of level d's slots, as ring items
+    if (E > sd.cap) E = sd.cap;
+    const uint32_t lo = (uint32_t)(((unsigned long long)E * gid) / nw),
+                   hi = (uint32_t)(((unsigned long long)E * (gid + 1)) / nw);
+    const uint32_t n = hi - lo;
+    constexpr uint32_t kMax = CAP / 2;
+    if (n > kMax) {  // (never with the host's target: a share far below a ring)
+        if (lane == 0) dev_error(err, kErrStackOverflow);
+        return 0;
+    }
+    const uint32_t *src = buf(d);
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + (uint32_t)lane;
+        uint4 a, c;
+        ld_sc1_x4x2(src + (size_t)(lo + (i < n ? i : 0u)) * W, a, c);
+        if (i < n) {
+            const uint32_t w[W] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+            store_tmpl<Kind, CAP>(st, i, w);
+            st.d[i] = make_uint2(w[W - 2], w[W - 1]);
+        }
+    }
+    return n;
+}
+
 // GLOBAL: the launch shares work with the other ranks through g->gview
 // (idle waves take chunks from the global ring, a wave holding spill_lo+
 // items exports a chunk while some rank is idle and none of its own waves
@@ -1137,6 +1366,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     Timeline tl;
     tl.init(g, gid);
     tl.log(kTlStart, 0);
+    ProbeStats pstat;
     uint32_t bot = 0, top = 0;
     bool active = false;
     uint32_t spins = 0;
@@ -1163,7 +1393,22 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
 #pragma unroll
     for (int i = 0; i < TW; ++i) ctmpl[i] = 0;
 
-    if (seed_roots) {
+    bool seeded = false;
+    if constexpr (Kind::kPure && Kind::kTmplWords == 6 && Kind::kWords == 8 && CAP >= 128) {
+        if (g->seed.buf) {
+            // breadth-first seeding: every wave starts with its share of the
+            // tree's top levels (the host set outstanding = every wave)
+            seeded = true;
+            top = seed_levels<Kind, CAP>(ctx, acc, g, st, gid, cfg.nwaves, cfg.spin_limit, n_exec, n_spawn, nbatch, tl);
+            active = true;
+            tl.log(kTlBusy, top);
+            if (top == 0) {
+                active = false;
+                wave_goes_idle<GLOBAL>(g, gv, pool);
+            }
+        }
+    }
+    if (seed_roots && !seeded) {
         uint32_t tmpl[TW];
         const int n = Kind::roots(ctx, acc, tmpl);  // uniform across the wave
         uint32_t ucnt = lane == 0 && n > 0 ? (uint32_t)n : 0u;
@@ -1244,7 +1489,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             }
             uint32_t fin = 0;
             if (n == 0) {
-                n = dequeue_chunk<Kind, CAP>(pool, q, st, g, fin);
+                n = dequeue_chunk<Kind, CAP>(pool, q, st, g, fin, pstat);
                 src = q == home ? 1 : 2;
             }
             if constexpr (!GLOBAL) {
@@ -1608,9 +1853,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         const uint32_t lo = spill_lo_now(cfg, hungry);
         if (sz > cfg.spill_hi || (hungry > 0 && sz >= lo)) {
             const unsigned long long ts = __builtin_amdgcn_s_memtime();
+            const uint32_t cmax = (cfg.ramp_chunk && hungry * 8u > cfg.nwaves) ? cfg.ramp_chunk : pool.chunk;
             while (sz > cfg.spill_hi || (hungry > 0 && sz >= lo)) {
                 uint32_t n = (sz + 1) / 2;
-                if (n > pool.chunk) n = pool.chunk;
+                if (n > cmax) n = cmax;
                 if (n == 0 || n == sz) break;
                 // home deque first, then the other deques of this XCD slice
                 bool ok = false;
@@ -1624,9 +1870,22 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     }
                 }
                 if (!ok) publish_pending<Kind, CAP>(pool, g, pend);  // one deferred chunk at a time
+                // where the chunk goes: cfg.spread 0 = the home deque first, then the
+                // XCD's others; 1 = the XCD's deques in turn (chunk after chunk), so
+                // idle waves probing their own home deques find work without all
+                // converging on one deque's head; 2 = as 1, and over every XCD's
+                // deques while more than 1/8 of the waves are hungry (a ramp-up
+                // from one root reaches the other XCDs' idle waves at once)
+                // (cfg.defer 2: publish at once while many waves are hungry — a
+                // consumer that claims the ticket waits for the publish, on
+                // average a whole producer batch, profiles/r04 probe stats)
+                const bool defer_now = cfg.defer == 1 || (cfg.defer == 2 && hungry * 8u <= cfg.nwaves);
+                const uint32_t rot = cfg.spread ? npush : 0u;
+                const bool wide = cfg.spread > 1 && hungry * 8u > cfg.nwaves;
                 for (uint32_t a = 0; a < qpx && !ok; ++a) {
-                    const uint32_t q = xcc * qpx + (home - xcc * qpx + a) % qpx;
-                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, q, st, bot, n, occ, cfg.defer ? &pend : nullptr);
+                    const uint32_t q = wide ? (home + (rot + a) * (qpx + 1u)) % pool.nq
+                                            : xcc * qpx + (home - xcc * qpx + rot + a) % qpx;
+                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, q, st, bot, n, occ, defer_now ? &pend : nullptr);
                 }
                 if (!ok) break;  // deques full: keep the items (the ring still has room)
                 ++npush;
@@ -1762,6 +2021,13 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         }
     }
     tl.log(kTlEnd, 0);
+    if (HX_TIMELINE) {
+        auto sat = [](uint32_t v) { return v / 16u > 0xffffu ? 0xffffu : v / 16u; };
+        tl.log(kTlProbe, 0u << 16 | sat(pstat.probes));
+        tl.log(kTlProbe, 1u << 16 | sat(pstat.empty));
+        tl.log(kTlProbe, 2u << 16 | sat(pstat.lost));
+        tl.log(kTlProbe, 3u << 16 | sat(pstat.wait_us));
+    }
 }
 
 }  // namespace hx

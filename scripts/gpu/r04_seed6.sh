@@ -1,0 +1,10 @@
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out/r04
+export TMPDIR=/tmp HCLIB_HIP_SPIN_LIMIT_MS=5000
+timeout -k 10 300 python -u scripts/sweep_uts.py T1 HCLIB_HIP_SPILL_LO=336,400,448 HCLIB_HIP_WAVES_PER_CU=4,8 > gpurun_out/r04/seed6_t1.log 2>&1 &&
+timeout -k 10 300 python -u scripts/sweep_uts.py T1L HCLIB_HIP_SPILL_LO=336,400,448 > gpurun_out/r04/seed6_t1l.log 2>&1 &&
+timeout -k 10 300 python -u scripts/sweep_uts.py T1XL HCLIB_HIP_SPILL_LO=336,400,448 > gpurun_out/r04/seed6_t1xl.log 2>&1 &&
+timeout -k 10 300 python -u scripts/sweep_uts.py T1XL:7 HCLIB_HIP_SPILL_LO=336,400,448 > gpurun_out/r04/seed6_t1xl7.log 2>&1 &&
+echo ok

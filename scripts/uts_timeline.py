@@ -65,6 +65,33 @@ def summarise(tl, kernel_ms, bins=100):
             lo, hi = max(a, i * width), min(b, (i + 1) * width)
             if hi > lo:
                 curve[i] += (hi - lo) / width
+    # chunks given away (spill) and taken (busy from a deque / inbox) per bin,
+    # and the chunks queued at each bin's end: queued work with idle workers
+    # means discovery is slow; none queued means production is
+    gave, took = [0] * bins, [0] * bins
+    for w in tl:
+        for t, ev, val in w:
+            i = min(bins - 1, int(us(t) / width))
+            if ev == 4:
+                gave[i] += 1
+            elif ev == 2 and (val >> 16) in (1, 2, 3, 4):
+                took[i] += 1
+    # seeding levels: when the first / last worker saw each level complete
+    seed = {}
+    for w in tl:
+        for t, ev, val in w:
+            if ev == 8:
+                a, b = seed.get(val, (1e18, 0))
+                seed[val] = (min(a, us(t)), max(b, us(t)))
+    probe = [0, 0, 0, 0]  # probes, empty deques, lost CASes, publish-wait us (each x16)
+    for w in tl:
+        for t, ev, val in w:
+            if ev == 7:
+                probe[val >> 16] += 16 * (val & 0xFFFF)
+    queued, q = [], 0
+    for i in range(bins):
+        q += gave[i] - took[i]
+        queued.append(q)
     # per worker: termination seen / exit / last busy->idle / the event before termination
     per = []
     for w in tl:
@@ -89,6 +116,9 @@ def summarise(tl, kernel_ms, bins=100):
         "term_seen_us": [min(terms), max(terms)] if terms else None,
         "last_exit_us": end, "busy_worker_us": busy_us, "mean_active": busy_us / end if end else 0,
         "spills": spills, "bin_us": width, "active_per_bin": [round(c, 1) for c in curve],
+        "seed_levels_us": {int(k): [round(v[0], 2), round(v[1], 2)] for k, v in sorted(seed.items())},
+        "probes": dict(zip(("probes", "empty", "lost_cas", "publish_wait_us"), probe)),
+        "gave_per_bin": gave, "took_per_bin": took, "queued_per_bin": queued,
         "term_quantiles_us": {q: tq(q) for q in (0.0, 0.5, 0.9, 0.99, 1.0)},
         "exit_cost_us": {q: exit_cost[min(len(exit_cost) - 1, int(q * len(exit_cost)))] for q in (0.5, 0.9, 1.0)}
         if exit_cost else None,
@@ -130,7 +160,7 @@ def main():
                       "held", s["first_work_us"], "done", round(s["last_item_done_us"], 1), "term",
                       s["term_seen_us"], "exit", round(s["last_exit_us"], 1), "mean_active",
                       round(s["mean_active"], 1), "term_q", s["term_quantiles_us"], "exit_cost",
-                      s["exit_cost_us"], flush=True)
+                      s["exit_cost_us"], "probes", s["probes"], flush=True)
             assert tot == nodes, (name, tot, nodes)
 
 
