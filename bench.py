@@ -335,6 +335,17 @@ def cpu_baseline(allot, min_seconds=10.0):
     out.update({k: allot[k] for k in ("affinity_cpus", "cgroup_quota", "cgroup_source", "cpuset",
                                       "omp_num_threads", "host_cpus_visible", "allowed_cpus",
                                       "threads_source")})
+    # provenance of the port as a baseline: the
+    # reference runtime is not built here; the round-3 review built it and
+    # timed it beside this port on T3L
+    out["reference_cross_check"] = {
+        "source": "round-3 review (VERDICT.md): reference built out of tree with its CMake, test/uts/UTS.cpp "
+                  "with the survey's driver shims, T3L, same container",
+        "reference_nodes_per_s_8_workers": [22.6e6, 24.4e6], "port_nodes_per_s_8_workers": [35.5e6, 40.2e6],
+        "reference_nodes_per_s_1_worker": 3.88e6, "port_nodes_per_s_1_worker": 3.9e6,
+        "port_over_reference_8_workers": 1.6,
+        "note": "the port is the faster CPU baseline: GPU/CPU ratios against it understate the GPU's lead "
+                "over the reference runtime"}
     return out
 
 

@@ -13,6 +13,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <type_traits>
 #include <vector>
 
 #include "hx_module.h"
@@ -178,6 +179,11 @@ struct UtsKind {
     static constexpr bool kPure = true;
     static constexpr bool kBoundedChildren = true;  // <= 100 (the root goes through roots())
     using Ctx = UtsCtx;
+    // BIN trees: a node has m children or none (the narrow loop's fast path;
+    // hx_sched.h KindFixedChildren). Sharded BIN searches drop foreign nodes
+    // (0 children) at the split: still none-or-m.
+    static constexpr bool kFixedChildren = MODE == kUtsBin;
+    __device__ static uint32_t fixed_children(const Ctx &c) { return c.m > 0 ? (uint32_t)c.m : 0u; }
     struct Acc {
         // per lane: at most one node per batch, so 32 bits last 4G batches
         uint32_t nodes = 0, leaves = 0;

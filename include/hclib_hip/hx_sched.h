@@ -333,6 +333,19 @@ struct KindHasDual<K, decltype((void)&K::process2)> {
 };
 template <class K>
 constexpr int group_max_of() { return KindPieces<K>::value + 2; }  // items one lane pushes per batch
+// Optional: static uint32_t fixed_children(const Ctx&) — every task has either
+// no children or exactly this many (<= the Kind's pieces; UTS BIN trees: m):
+// the narrow loop then skips its uniformity test and reads no group size
+// (declared with static constexpr bool kFixedChildren = true; a return of 0
+// or more than the pieces falls back to the general test)
+template <class K, class = void>
+struct KindFixedChildren {
+    static constexpr bool value = false;
+};
+template <class K>
+struct KindFixedChildren<K, decltype((void)K::kFixedChildren)> {
+    static constexpr bool value = K::kFixedChildren;
+};
 constexpr uint32_t kMaxChildren = 1u << 24;  // kend shares its descriptor word with delta
 
 template <class Kind, int CAP>
@@ -797,18 +810,20 @@ __device__ __forceinline__ uint32_t rcp16(uint32_t mu) {
 // template to lane o.
 template <int TW>
 __device__ __forceinline__ void carry_permute(unsigned long long spawn, uint32_t mu, uint32_t nch,
-                                              const uint32_t *child, uint32_t *ctmpl, uint32_t &ck) {
+                                              const uint32_t *child, uint32_t *ctmpl, uint32_t &ck,
+                                              uint32_t rcp = 0) {
     const uint32_t lane = (uint32_t)lane_id();
     const uint32_t nsp = (uint32_t)__builtin_popcountll(spawn);
     const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(spawn >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
     const uint32_t dst = nch != 0 ? rk : nsp + (lane - rk);
     const int src_of_rank = __builtin_amdgcn_ds_permute((int)(dst * 4u), (int)lane);
-    const uint32_t r = (lane * rcp16(mu)) >> 16;  // lane / mu (lane < 64, mu <= 8)
+    // lane / mu (lane < 64, mu <= 8); 24-bit multiplies issue at full rate
+    const uint32_t r = __umul24(lane, rcp ? rcp : rcp16(mu)) >> 16;
     const int src = __builtin_amdgcn_ds_bpermute((int)(r * 4u), src_of_rank);
 #pragma unroll
     for (int i = 0; i < TW; ++i) ctmpl[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(src * 4, (int)child[i]);
-    ck = lane - r * mu;
+    ck = lane - __umul24(r, mu);
 }
 
 // Uniform push: no lane has a residual range and every lane that spawned a
@@ -980,6 +995,14 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
     acc_set_mode(acc, 1u);
     const uint32_t lane = (uint32_t)lane_id();
     uint32_t carry = lane0(ns.carry), batches = 0;
+    // fixed-size families (KindFixedChildren): the group size and its
+    // reciprocal are loop invariants
+    uint32_t mu_fix = 0, rcp_fix = 0;
+    if constexpr (KindFixedChildren<Kind>::value) {
+        mu_fix = lane0(Kind::fixed_children(ctx));
+        if (mu_fix > (uint32_t)kPieces) mu_fix = 0;
+        rcp_fix = mu_fix ? rcp16(mu_fix) : 0u;
+    }
     while (true) {
         const bool h = lane < carry;
         uint32_t ch2[TW];
@@ -1003,12 +1026,21 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
             carry = 0;
             break;
         }
-        const uint32_t mu2 = (uint32_t)__builtin_amdgcn_readlane((int)n2, __builtin_ctzll(sp2));
-        const bool uni2 = __ballot(u2 > (uint32_t)kPieces || (n2 != 0 && n2 != mu2)) == 0;
+        uint32_t mu2;
+        bool uni2;
+        if (KindFixedChildren<Kind>::value && mu_fix) {
+            mu2 = mu_fix;
+            uni2 = true;
+        } else {
+            mu2 = (uint32_t)__builtin_amdgcn_readlane((int)n2, __builtin_ctzll(sp2));
+            uni2 = __ballot(u2 > (uint32_t)kPieces || (n2 != 0 && n2 != mu2)) == 0;
+        }
         if (uni2) {
             const uint32_t t2 = mu2 * (uint32_t)__builtin_popcountll(sp2);
             if (t2 <= (uint32_t)kWaveSize) {
-                carry_permute<TW>(sp2, mu2, n2, ch2, ns.ctmpl, ns.ck);
+                // (a scalar walk over the spawn mask instead of the permute pair
+                // measured slower: T3L 31.8 -> 32.6 ms, profiles/r04/walk_ab.log)
+                carry_permute<TW>(sp2, mu2, n2, ch2, ns.ctmpl, ns.ck, rcp_fix);
                 carry = t2;
                 continue;
             }
