@@ -22,12 +22,15 @@ namespace hx {
 struct FibCtx {
     int n;
     int local;  // scopes in the wave's LDS while they stay inside it (hx_finish.h LocalScopes)
+    int blocks; // HBM scope ids taken kScopeBlock at a time per wave
     FinishArena fin;
 };
 
 // the wave's LDS finish scopes (file scope: every access is a ds_* op)
 constexpr int kFibLocalScopes = 512;
 __shared__ LocalScopes<kFibLocalScopes> s_fib_scopes;
+// the wave's block of HBM scope ids (hx_finish.h finish_open `blk`)
+__shared__ uint32_t s_fib_blk[2];
 
 struct FibKind {
     // template = {n + 1 of the parent call, the parent's scope}; child k is
@@ -59,8 +62,9 @@ struct FibKind {
         const bool spawn = n >= 2;
         // FINISH { async fib(n-1); async fib(n-2); }  (one bump allocation
         // per wave for every lane that opens a scope)
-        const uint32_t j = c.local ? finish_open_local(c.fin, s_fib_scopes, spawn, t[1], 2, 0, err)
-                                   : finish_open(c.fin, spawn, t[1], 2, 0, err);
+        const uint32_t j = c.local ? finish_open_local(c.fin, s_fib_scopes, spawn, t[1], 2, 0, err,
+                                                       c.blocks ? s_fib_blk : nullptr)
+                                   : finish_open(c.fin, spawn, t[1], 2, 0, err, c.blocks ? s_fib_blk : nullptr);
         if (!spawn) {  // a leaf returns n: check out, continuations inline
             acc.joins += c.local ? finish_check_out_local(c.fin, s_fib_scopes, t[1], (unsigned long long)n, PassSum())
                                  : finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
@@ -86,6 +90,8 @@ __global__ __launch_bounds__(64) void k_fib(FibCtx ctx, PoolView pool, SchedGlob
                                             SchedConfig cfg) {
     __shared__ WaveStack<FibKind, kFibCap> st;
     if (ctx.local) s_fib_scopes.init();
+    if (threadIdx.x < 2) s_fib_blk[threadIdx.x] = 0;
+    __syncthreads();
     run_worker<FibKind, kFibCap>(ctx, pool, g, cfg, st, blockIdx.x == 0);
 }
 
@@ -112,7 +118,16 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
         set_error("hclib_hip_fib: n too large for the join arena");
         return HCLIB_HIP_EINVAL;
     }
-    const size_t jb = sizeof(FinishScope) * (size_t)(scopes + 1);
+    const int grid = env_int("HCLIB_HIP_GRID", 0) > 0 ? env_int("HCLIB_HIP_GRID", 0)
+                                                    : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 2);
+    const int blocks = env_int("HCLIB_HIP_FIB_BLOCKS", 1);
+    // the arena: every scope once, plus each wave's last partly used id block
+    const unsigned long long ids = scopes + 1 + (blocks ? (unsigned long long)grid * kScopeBlock : 0ull);
+    if (ids > 0xfffffff0ull) {
+        set_error("hclib_hip_fib: n too large for the join arena");
+        return HCLIB_HIP_EINVAL;
+    }
+    const size_t jb = sizeof(FinishScope) * (size_t)ids;
     void *dmem = nullptr;
     HX_HIP(hipMalloc(&dmem, jb + 512));
     FibCtx ctx;
@@ -120,7 +135,8 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     ctx.local = env_int("HCLIB_HIP_FIB_LOCAL", 0);  // LDS scopes: measured slower so far (profiles/r04/fib_stamps.log)
     ctx.fin.scopes = (FinishScope *)dmem;
     ctx.fin.next = (uint32_t *)((char *)dmem + ((jb + 255) & ~(size_t)255));
-    ctx.fin.cap = (uint32_t)(scopes + 1);
+    ctx.fin.cap = (uint32_t)ids;
+    ctx.blocks = blocks;
     ctx.fin.root_value = (unsigned long long *)(ctx.fin.next + 16);
     HX_HIP(hipMemsetAsync(ctx.fin.next, 0, 256, m.stream));
     PoolView pool;
@@ -130,8 +146,6 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
                      // (profiles/r02/fib_knobs.log; 8-item chunks made the 2,048
                      // idle-polling waves of the old default fight over crumbs)
                      (uint32_t)env_int("HCLIB_HIP_FIB_CHUNK", 32), FibKind::kWords, &pool));
-    const int grid = env_int("HCLIB_HIP_GRID", 0) > 0 ? env_int("HCLIB_HIP_GRID", 0)
-                                                    : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 2);
     SchedConfig cfg;
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_HI", 256);
     // scripts/sweep_uts.py fib30 (profiles/r01_s5/knob_sweeps.log): 32 -> 1.50 ms, 2 -> 1.70 ms

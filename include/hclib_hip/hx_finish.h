@@ -48,17 +48,47 @@ struct FinishArena {
 // `parent`; returns the lane's scope id (kScopeRoot for lanes that do not
 // open one, or on arena exhaustion, which is reported through err).
 // Called by the whole wave.
+// `blk` (optional): two words of the calling wave's LDS, {next, end} of a
+// block of scope ids the wave took from the arena (kScopeBlock at a time, one
+// agent atomic per block instead of one per open), zeroed before its first
+// open. Wave-uniform state in LDS, not in registers: a lane inactive at an
+// update would keep a stale register copy (divergent batches).
+constexpr uint32_t kScopeBlock = 256;
 __device__ __forceinline__ uint32_t finish_open(const FinishArena &a, bool open, uint32_t parent, uint32_t count,
-                                                uint32_t cont, uint32_t *err) {
+                                                uint32_t cont, uint32_t *err, uint32_t *blk = nullptr) {
     const unsigned long long m = __ballot(open);
     if (!m) return kScopeRoot;
     const int leader = __builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane_id() == leader) base = add_agent(a.next, (uint32_t)__popcll(m));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    const uint32_t k = (uint32_t)__popcll(m);
+    const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    uint32_t s = 0;
+    if (blk && k <= kScopeBlock) {
+        // the rest of the current block first, then a new block (ids need not
+        // be contiguous: only the last block of each wave leaves ids unused)
+        const uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)blk[0]),
+                       end = (uint32_t)__builtin_amdgcn_readfirstlane((int)blk[1]);
+        const uint32_t left = end - nxt;
+        if (k <= left) {
+            s = nxt + rank;
+            if (lane_id() == leader) blk[0] = nxt + k;
+        } else {
+            uint32_t b = 0;
+            if (lane_id() == leader) b = add_agent(a.next, kScopeBlock);
+            b = (uint32_t)__builtin_amdgcn_readlane((int)b, leader);
+            s = rank < left ? nxt + rank : b + (rank - left);
+            if (lane_id() == leader) {
+                blk[0] = b + (k - left);
+                blk[1] = b + kScopeBlock;
+            }
+        }
+        asm volatile("" ::: "memory");
+    } else {
+        uint32_t base = 0;
+        if (lane_id() == leader) base = add_agent(a.next, k);
+        s = (uint32_t)__builtin_amdgcn_readlane((int)base, leader) + rank;
+    }
     if (!open) return kScopeRoot;
-    const uint32_t s = base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     if (s >= a.cap || count == 0 || count > 255) {
         dev_error(err, s >= a.cap ? kErrArena : kErrBadTask);
         return kScopeRoot;
@@ -81,6 +111,9 @@ __device__ __forceinline__ uint32_t finish_check_out(const FinishArena &a, uint3
     while (s != kScopeRoot) {
         if (s >= a.cap) return ran;  // (never: an LDS or stale id here would be a protocol bug, not a fault)
         FinishScope *f = &a.scopes[s];
+        // {parent, cont} never change after the open: loaded beside the
+        // check-out (one round trip per chain step, not two)
+        const unsigned long long pc = ld_agent((const unsigned long long *)&f->parent);
         unsigned long long old = add_agent(&f->word, v - kScopeOne), add = v;
         if ((old & kScopeSumMask) + v > kScopeSumMask) {
             // the sum carried into the count byte: take the carry back out with
@@ -92,10 +125,9 @@ __device__ __forceinline__ uint32_t finish_check_out(const FinishArena &a, uint3
         }
         if ((old >> 56) != 1) return ran;  // a sibling is still running
         const unsigned long long sum = (old + add) & kScopeSumMask;
-        const uint32_t cw = ld_agent(&f->cont);
-        v = cont(cw, sum) & kScopeSumMask;
+        v = cont((uint32_t)(pc >> 32), sum) & kScopeSumMask;
         ++ran;
-        s = ld_agent(&f->parent);
+        s = (uint32_t)pc;
     }
     st_agent(a.root_value, v);
     return ran;
@@ -124,18 +156,23 @@ constexpr uint32_t kScopeLds = 0x40000000u;  // scope id bit: an LDS slot of the
 template <int N>
 struct LocalScopes {
     unsigned long long word[N];  // live tasks << 56 | sum (as FinishScope::word)
-    uint32_t parent[N];
-    uint32_t cont[N];
-    uint32_t fwd[N];       // 0, or 1 + the HBM scope this slot was promoted to
+    // {parent, cont, fwd, mark}: fwd = 0, or 1 + the HBM scope this slot was
+    // promoted to; mark = the promotion round that last visited the slot.
+    // One 16-byte LDS read per check-out step, issued beside its atomic
+    hx_u32x4 meta[N];
     uint32_t freelist[N];
     uint32_t nfree;
+    uint32_t epoch;  // promotion rounds (finish_promote)
     // every lane of the wave calls init once before the first open
     __device__ void init() {
         for (int i = lane_id(); i < N; i += 64) {
             freelist[i] = (uint32_t)(N - 1 - i);
-            fwd[i] = 0;
+            meta[i] = hx_u32x4{kScopeRoot, 0u, 0u, 0u};
         }
-        if (lane_id() == 0) nfree = N;
+        if (lane_id() == 0) {
+            nfree = N;
+            epoch = 0;
+        }
         asm volatile("" ::: "memory");
     }
 };
@@ -143,42 +180,67 @@ struct LocalScopes {
 __device__ __forceinline__ bool scope_is_lds(uint32_t s) { return s != kScopeRoot && (s & kScopeLds); }
 
 // The scope a lane's exported item must name: its LDS scope promoted to HBM
-// (with every unpromoted LDS ancestor, top-most first), or `s` itself.
-// Called by the whole wave.
+// (with every unpromoted LDS ancestor), or `s` itself. All scopes one call
+// promotes take ONE arena allocation: every lane marks the unpromoted slots
+// on its chain (round `epoch`), the wave numbers the marked slots, takes that
+// many HBM ids with one atomic, forwards each slot and writes its HBM copy
+// (parents resolved through the forwards just set). Called by the whole wave.
 template <int N>
 __device__ __forceinline__ uint32_t finish_promote(const FinishArena &a, LocalScopes<N> &ls, uint32_t s,
                                                    uint32_t *err) {
+    const int lane = lane_id();
     const int lead = __builtin_ctzll(__ballot(1));  // the first active lane does the scalar work
-    auto unpromoted = [&](uint32_t x) { return scope_is_lds(x) && ls.fwd[x & (kScopeLds - 1)] == 0; };
-    auto resolve = [&](uint32_t x) { return scope_is_lds(x) ? ls.fwd[x & (kScopeLds - 1)] - 1 : x; };
-    for (int guard = 0; guard < 4 * N + 64; ++guard) {
-        const unsigned long long m = __ballot(unpromoted(s));
-        if (!m) break;
-        // the top-most unpromoted ancestor of the first such lane's scope
-        uint32_t top = (uint32_t)__builtin_amdgcn_readlane((int)s, __builtin_ctzll(m));
-        for (int d = 0; d < N; ++d) {
-            const uint32_t p = ls.parent[top & (kScopeLds - 1)];
-            if (!unpromoted(p)) break;
-            top = p;
-        }
-        top = (uint32_t)__builtin_amdgcn_readfirstlane((int)top);
-        const uint32_t slot = top & (kScopeLds - 1);
-        uint32_t h = 0;
-        if (lane_id() == lead) h = add_agent(a.next, 1u);
-        h = (uint32_t)__builtin_amdgcn_readfirstlane((int)h);
-        if (h >= a.cap) {
-            if (lane_id() == lead) dev_error(err, kErrArena);
-            return kScopeRoot;
-        }
-        if (lane_id() == lead) {
-            FinishScope *f = &a.scopes[h];
-            st_agent(&f->word, ls.word[slot]);
-            st_agent(&f->parent, resolve(ls.parent[slot]));
-            st_agent(&f->cont, ls.cont[slot]);
-            ls.fwd[slot] = h + 1;
-        }
-        asm volatile("" ::: "memory");
+    constexpr uint32_t kMask = kScopeLds - 1;
+    auto unpromoted = [&](uint32_t x) { return scope_is_lds(x) && ls.meta[x & kMask].z == 0; };
+    auto resolve = [&](uint32_t x) { return scope_is_lds(x) ? ls.meta[x & kMask].z - 1 : x; };
+    if (!__ballot(unpromoted(s))) return resolve(s);
+    const uint32_t ep = (uint32_t)__builtin_amdgcn_readfirstlane((int)ls.epoch) + 1u;
+    // 1. mark every unpromoted slot on every lane's chain
+    for (uint32_t x = s; unpromoted(x);) {
+        hx_u32x4 *m = &ls.meta[x & kMask];
+        if (m->w == ep) break;  // another lane's walk got here first
+        m->w = ep;
+        x = m->x;
     }
+    asm volatile("" ::: "memory");
+    // 2. number the marked slots (slot i by lane i % 64), one allocation
+    constexpr int kPer = (N + 63) / 64;
+    uint32_t mine = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int i = lane + 64 * q;
+        mine += (i < N && ls.meta[i].w == ep && ls.meta[i].z == 0) ? 1u : 0u;
+    }
+    const int P = wave_incl_scan((int)mine);
+    const uint32_t tot = (uint32_t)__shfl(P, 63, 64);
+    uint32_t base = 0;
+    if (lane == lead) base = add_agent(a.next, tot);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+    if (base + tot > a.cap) {
+        if (lane == lead) dev_error(err, kErrArena);
+        return kScopeRoot;
+    }
+    uint32_t h = base + (uint32_t)P - mine;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int i = lane + 64 * q;
+        if (i < N && ls.meta[i].w == ep && ls.meta[i].z == 0) ls.meta[i].z = 1u + h++;
+    }
+    asm volatile("" ::: "memory");
+    // 3. the HBM copies (every parent is now root, HBM or forwarded)
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int i = lane + 64 * q;
+        if (i < N && ls.meta[i].w == ep) {
+            const hx_u32x4 m = ls.meta[i];
+            FinishScope *f = &a.scopes[m.z - 1];
+            st_agent(&f->word, ls.word[i]);
+            st_agent(&f->parent, resolve(m.x));
+            st_agent(&f->cont, m.y);
+        }
+    }
+    if (lane == lead) ls.epoch = ep;
+    asm volatile("" ::: "memory");
     return resolve(s);
 }
 
@@ -186,7 +248,8 @@ __device__ __forceinline__ uint32_t finish_promote(const FinishArena &a, LocalSc
 // scope while the free list lasts, the rest HBM scopes (finish_open).
 template <int N>
 __device__ __forceinline__ uint32_t finish_open_local(const FinishArena &a, LocalScopes<N> &ls, bool open,
-                                                      uint32_t parent, uint32_t count, uint32_t cont, uint32_t *err) {
+                                                      uint32_t parent, uint32_t count, uint32_t cont, uint32_t *err,
+                                                      uint32_t *blk = nullptr) {
     const unsigned long long m = __ballot(open);
     if (!m) return kScopeRoot;
     const uint32_t k = (uint32_t)__popcll(m);
@@ -196,7 +259,7 @@ __device__ __forceinline__ uint32_t finish_open_local(const FinishArena &a, Loca
         // the free list ran dry: HBM scopes, whose parents must be HBM scopes
         // too (another wave may close them and check out of their parent)
         const uint32_t par = finish_promote(a, ls, open ? parent : kScopeRoot, err);
-        return finish_open(a, open, par, count, cont, err);
+        return finish_open(a, open, par, count, cont, err, blk);
     }
     const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -204,9 +267,7 @@ __device__ __forceinline__ uint32_t finish_open_local(const FinishArena &a, Loca
     if (open) {
         const uint32_t slot = ls.freelist[nf - 1 - rank];
         ls.word[slot] = (unsigned long long)count << 56;
-        ls.parent[slot] = parent;
-        ls.cont[slot] = cont;
-        ls.fwd[slot] = 0;
+        ls.meta[slot] = hx_u32x4{parent, cont, 0u, 0u};
         s = kScopeLds | slot;
     }
     if (lane_id() == __builtin_ctzll(m)) ls.nfree = nf - k;  // (lane 0 may be inactive: an open lane)
@@ -216,7 +277,9 @@ __device__ __forceinline__ uint32_t finish_open_local(const FinishArena &a, Loca
 
 // finish_check_out over LDS and HBM scopes (a chain may cross from the
 // wave's LDS into HBM, never back: an HBM scope's parent is never an
-// unpromoted LDS slot)
+// unpromoted LDS slot). One LDS round trip per LDS step: the slot's meta
+// read is issued beside its atomic (a forwarded slot's word is dead, so the
+// stray add there is harmless).
 template <int N, class Cont>
 __device__ __forceinline__ uint32_t finish_check_out_local(const FinishArena &a, LocalScopes<N> &ls, uint32_t s,
                                                            unsigned long long value, Cont &&cont) {
@@ -226,14 +289,14 @@ __device__ __forceinline__ uint32_t finish_check_out_local(const FinishArena &a,
         if (!scope_is_lds(s)) return ran + finish_check_out(a, s, v, cont);
         const uint32_t slot = s & (kScopeLds - 1);
         if (slot >= (uint32_t)N) return ran;  // (never; see finish_check_out)
-        const uint32_t f = ls.fwd[slot];
-        if (f) {  // promoted: the HBM copy counts from here on
-            s = f - 1;
-            continue;
-        }
+        const hx_u32x4 meta = ls.meta[slot];
         unsigned long long old = __hip_atomic_fetch_add(&ls.word[slot], v - kScopeOne, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_WORKGROUP),
                            add = v;
+        if (meta.z) {  // promoted: the HBM copy counts from here on
+            s = meta.z - 1;
+            continue;
+        }
         if ((old & kScopeSumMask) + v > kScopeSumMask) {  // see finish_check_out
             old = __hip_atomic_fetch_add(&ls.word[slot], (unsigned long long)0 - kScopeOne, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -241,13 +304,12 @@ __device__ __forceinline__ uint32_t finish_check_out_local(const FinishArena &a,
         }
         if ((old >> 56) != 1) return ran;
         const unsigned long long sum = (old + add) & kScopeSumMask;
-        const uint32_t cw = ls.cont[slot], par = ls.parent[slot];
         // the slot is free again
         const uint32_t pos = __hip_atomic_fetch_add(&ls.nfree, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ls.freelist[pos] = slot;
-        v = cont(cw, sum) & kScopeSumMask;
+        v = cont(meta.y, sum) & kScopeSumMask;
         ++ran;
-        s = par;
+        s = meta.x;
     }
     st_agent(a.root_value, v);
     return ran;
