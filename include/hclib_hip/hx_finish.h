@@ -163,6 +163,7 @@ struct LocalScopes {
     uint32_t freelist[N];
     uint32_t nfree;
     uint32_t epoch;  // promotion rounds (finish_promote)
+    uint32_t cnt;    // finish_promote's slot count
     // every lane of the wave calls init once before the first open
     __device__ void init() {
         for (int i = lane_id(); i < N; i += 64) {
@@ -203,16 +204,19 @@ __device__ __forceinline__ uint32_t finish_promote(const FinishArena &a, LocalSc
         x = m->x;
     }
     asm volatile("" ::: "memory");
-    // 2. number the marked slots (slot i by lane i % 64), one allocation
-    constexpr int kPer = (N + 63) / 64;
+    // 2. number the marked slots, one allocation. The active lanes (any
+    // subset: export hooks run under divergent control flow) take slots
+    // rank, rank + na, ...; each lane's range comes from an LDS counter
+    const unsigned long long act = __ballot(1);
+    const int na = __popcll(act);
+    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    if (lane == lead) ls.cnt = 0;
+    asm volatile("" ::: "memory");
     uint32_t mine = 0;
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        const int i = lane + 64 * q;
-        mine += (i < N && ls.meta[i].w == ep && ls.meta[i].z == 0) ? 1u : 0u;
-    }
-    const int P = wave_incl_scan((int)mine);
-    const uint32_t tot = (uint32_t)__shfl(P, 63, 64);
+    for (int i = rank; i < N; i += na) mine += (ls.meta[i].w == ep && ls.meta[i].z == 0) ? 1u : 0u;
+    const uint32_t off = __hip_atomic_fetch_add(&ls.cnt, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readfirstlane((int)ls.cnt);
     uint32_t base = 0;
     if (lane == lead) base = add_agent(a.next, tot);
     base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
@@ -220,18 +224,13 @@ __device__ __forceinline__ uint32_t finish_promote(const FinishArena &a, LocalSc
         if (lane == lead) dev_error(err, kErrArena);
         return kScopeRoot;
     }
-    uint32_t h = base + (uint32_t)P - mine;
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        const int i = lane + 64 * q;
-        if (i < N && ls.meta[i].w == ep && ls.meta[i].z == 0) ls.meta[i].z = 1u + h++;
-    }
+    uint32_t h = base + off;
+    for (int i = rank; i < N; i += na)
+        if (ls.meta[i].w == ep && ls.meta[i].z == 0) ls.meta[i].z = 1u + h++;
     asm volatile("" ::: "memory");
     // 3. the HBM copies (every parent is now root, HBM or forwarded)
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        const int i = lane + 64 * q;
-        if (i < N && ls.meta[i].w == ep) {
+    for (int i = rank; i < N; i += na) {
+        if (ls.meta[i].w == ep) {
             const hx_u32x4 m = ls.meta[i];
             FinishScope *f = &a.scopes[m.z - 1];
             st_agent(&f->word, ls.word[i]);

@@ -55,7 +55,9 @@ while t != 0:
                  "in_ingress": ns(tr[t, 8] - tr[t, 1]), "in_wave0": ns(tr[t, 10] - tr[t, 1]),
                  "in_wave1": ns(tr[t, 11] - tr[t, 1]), "in_egress": ns(tr[t, 9] - tr[t, 1]),
                  # waves 0 / 1: loop start (prologue done)
-                 "in_w0_loop": ns(tr[t, 12] - tr[t, 1]), "in_w1_loop": ns(tr[t, 15] - tr[t, 1])})
+                 "in_w0_loop": ns(tr[t, 12] - tr[t, 1]), "in_w1_loop": ns(tr[t, 15] - tr[t, 1]),
+                 # HCLIB_HIP_SW_PK=2 (sw_pk2_tile): wave B's inputs / first chunk (sweep end = in_w1_loop)
+                 "in_b_inputs": ns(tr[t, 13] - tr[t, 1]), "in_b_loop": ns(tr[t, 14] - tr[t, 1])})
     t = r
 hops.reverse()
 total = ns(tr[ntw * nth - 1, 2] - t0)
@@ -67,7 +69,7 @@ for kind in ("row", "col", "diag", "all"):
         continue
     res[kind] = {"hops": len(hs), "kept": sum(h["kept"] for h in hs)}
     for k in ("release", "pickup", "body", "put", "in_ingress", "in_w0_loop", "in_wave0", "in_w1_loop", "in_wave1",
-              "in_egress"):
+              "in_egress", "in_b_inputs", "in_b_loop"):
         v = np.array([h[k] for h in hs])
         res[kind][k + "_us"] = round(float(v.mean()) / 1e3, 3)
         res[kind][k + "_ms_total"] = round(float(v.sum()) / 1e6, 3)

@@ -294,6 +294,18 @@ def test_sw_64k_golden_on_generic_promise_dag(golden, monkeypatch):
     assert st["tiles"] == 65536
 
 
+@pytest.mark.parametrize("pk", ["1", "2"])
+def test_sw_64k_golden_on_packed_bodies(golden, pk, monkeypatch):
+    """SW-64K on the promise DAG with the one-sweep-wave (1) and the
+    two-sweep-wave (2) packed tile bodies: 128772."""
+    monkeypatch.setenv("HCLIB_HIP_SW_SCHED", "dag")
+    monkeypatch.setenv("HCLIB_HIP_SW_PK", pk)
+    s1, s2 = _sw_inputs("huge")
+    score, st = H.sw(s1[:65536], s2[:65536], 256, 256)
+    assert score == golden("sw_goldens.json")["sw64k"]["score"] == 128772
+    assert st["tiles"] == 65536
+
+
 @pytest.mark.parametrize("tw", [1, 30, 63, 64, 65, 100, 256, 300, 511, 512])
 def test_sw_dag_packed_half_tiles(tw, monkeypatch):
     """256-row tiles at most 512 wide run the promise DAG's packed-half body
@@ -315,6 +327,9 @@ def test_sw_dag_packed_half_tiles(tw, monkeypatch):
         assert score == want and st["tiles"] == (n1 // tw) * 3, (tw, score, want)
         monkeypatch.setenv("HCLIB_HIP_SW_PK", "0")
         assert H.sw(a, b, tw, 256)[0] == want
+        # the two-sweep-wave body (sw_pk2_tile)
+        monkeypatch.setenv("HCLIB_HIP_SW_PK", "2")
+        assert H.sw(a, b, tw, 256)[0] == want, (tw, "pk2")
         monkeypatch.delenv("HCLIB_HIP_SW_PK")
 
 
