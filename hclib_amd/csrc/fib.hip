@@ -22,6 +22,8 @@ namespace hx {
 struct FibCtx {
     int n;
     int local;  // scopes in the wave's LDS while they stay inside it (hx_finish.h LocalScopes)
+    int defer;  // HBM check-out steps issued in one batch, resolved in the next (finish_issue)
+    int climb;  // LDS mode: a leaf climbs its scope chain inline (else one level per task: kFibCont items)
     int blocks; // HBM scope ids taken kScopeBlock at a time per wave
     FinishArena fin;
 };
@@ -38,14 +40,21 @@ struct FibKind {
     static constexpr int kTmplWords = 2;
     static constexpr int kWords = 4;
     static constexpr bool kPure = false;           // scopes are opened / checked out in HBM
-    static constexpr bool kBoundedChildren = true;  // 0 or 2
+    static constexpr bool kBoundedChildren = true;  // 0, 1 (a continuation item) or 2
     using Ctx = FibCtx;
     struct Acc {
         unsigned long long tasks = 0, joins = 0;
+        FinishInFlight q;  // this lane's HBM check-out step in flight (FibCtx::defer)
+        // HX_STAMPS builds: cycles in process's phases (resolve, open, check-out), first active lane only
+        unsigned long long cyc[3] = {0, 0, 0};
         // the wave's totals go into its exit record (hx_sched.h Kind concept)
         __device__ void totals(unsigned long long (&c)[8], unsigned long long (&)[4]) {
             c[0] = wave_sum(tasks);
             c[1] = wave_sum(joins);
+#if defined(HX_STAMPS) && HX_STAMPS
+            c[2] = wave_sum(cyc[0] + cyc[1]);  // (the scheduler keeps c[4..7])
+            c[3] = wave_sum(cyc[2]);
+#endif
         }
     };
 
@@ -55,25 +64,125 @@ struct FibKind {
         return 1;
     }
 
+    // LDS mode: a scope's climb runs one level per task. The last task out of
+    // scope s pushes the continuation item {kFibCont, s} (its sum is in s's
+    // word), which frees s and checks out of s's parent in a later batch: a
+    // batch waits for one check-out per lane, not for its longest chain
+    static constexpr uint32_t kFibCont = 0xFFFFFFFFu;
+
+    // one check-out step of v from scope s; true: s's last task is out (LDS s)
+    __device__ static bool check_out_one(const Ctx &c, Acc &acc, uint32_t s, unsigned long long v) {
+        v &= kScopeSumMask;
+        if (s == kScopeRoot) {
+            st_agent(c.fin.root_value, v);
+            return false;
+        }
+        if (scope_is_lds(s)) {
+            const uint32_t slot = s & (kScopeLds - 1);
+            if (slot >= (uint32_t)kFibLocalScopes) return false;  // (never)
+            const hx_u32x4 meta = s_fib_scopes.meta[slot];
+            unsigned long long old = __hip_atomic_fetch_add(&s_fib_scopes.word[slot], v - kScopeOne, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (!meta.z) {
+                if ((old & kScopeSumMask) + v > kScopeSumMask)  // see finish_check_out
+                    old = __hip_atomic_fetch_add(&s_fib_scopes.word[slot], (unsigned long long)0 - kScopeOne,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return (old >> 56) == 1;
+            }
+            s = meta.z - 1;  // promoted: the HBM copy counts (the LDS add is harmless)
+        }
+        if (c.defer && acc.q.s == kScopeRoot) finish_issue(c.fin, acc.q, s, v);
+        else acc.joins += finish_check_out(c.fin, s, v, PassSum());
+        return false;
+    }
+
     __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
                                   uint32_t *child, uint32_t *err, bool) {
-        acc.tasks += 1;
-        const int n = (int)t[0] - 1 - (int)k;
-        const bool spawn = n >= 2;
+#if defined(HX_STAMPS) && HX_STAMPS
+        const bool lead = lane_id() == __builtin_ctzll(__ballot(1));
+        auto stamp = [&](int i, unsigned long long &ts) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            if (lead && i >= 0) acc.cyc[i] += now - ts;
+            ts = now;
+        };
+#else
+        auto stamp = [](int, unsigned long long &) {};
+#endif
+        unsigned long long tst = 0;
+        stamp(-1, tst);
+        // the HBM check-out this lane issued a batch ago: its result is in
+        if (c.defer) acc.joins += finish_resolve(c.fin, acc.q, PassSum());
+        stamp(0, tst);
+        const bool cont_item = c.local && !c.climb && t[0] == kFibCont;
+        const int n = cont_item ? 0 : (int)t[0] - 1 - (int)k;
+        const bool spawn = !cont_item && n >= 2;
+        if (!cont_item) acc.tasks += 1;
         // FINISH { async fib(n-1); async fib(n-2); }  (one bump allocation
         // per wave for every lane that opens a scope)
         const uint32_t j = c.local ? finish_open_local(c.fin, s_fib_scopes, spawn, t[1], 2, 0, err,
                                                        c.blocks ? s_fib_blk : nullptr)
                                    : finish_open(c.fin, spawn, t[1], 2, 0, err, c.blocks ? s_fib_blk : nullptr);
-        if (!spawn) {  // a leaf returns n: check out, continuations inline
-            acc.joins += c.local ? finish_check_out_local(c.fin, s_fib_scopes, t[1], (unsigned long long)n, PassSum())
+        stamp(1, tst);
+        if (spawn) {
+            if (j == kScopeRoot) return 0;  // arena error (reported)
+            child[0] = (uint32_t)n;  // children fib(n-1), fib(n-2)
+            child[1] = j;
+            return 2;
+        }
+        if (!c.local || c.climb) {  // a leaf returns n: check out, continuations inline
+            acc.joins += c.local ? finish_check_out_local(c.fin, s_fib_scopes, t[1], (unsigned long long)n, PassSum(),
+                                                          c.defer ? &acc.q : nullptr)
                                  : finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
+            stamp(2, tst);
             return 0;
         }
-        if (j == kScopeRoot) return 0;  // arena error (reported)
-        child[0] = (uint32_t)n;  // children fib(n-1), fib(n-2)
-        child[1] = j;
-        return 2;
+        // a leaf checks n out of its scope; a continuation item frees its
+        // scope and checks the scope's sum out of the parent
+        uint32_t s = t[1], slot = 0;
+        unsigned long long v = (unsigned long long)n;
+        bool freeing = false;
+        if (cont_item) {
+            uint32_t x = t[1];
+            if (scope_is_lds(x)) {
+                slot = x & (kScopeLds - 1);
+                const hx_u32x4 meta = s_fib_scopes.meta[slot < (uint32_t)kFibLocalScopes ? slot : 0];
+                if (meta.z) x = meta.z - 1;  // (promoted: the HBM copy holds the sum)
+                else {
+                    v = s_fib_scopes.word[slot] & kScopeSumMask;  // PassSum: cont(_, sum) = sum
+                    s = meta.x;
+                    freeing = true;
+                }
+            }
+            if (!freeing) {  // an HBM scope (an exported continuation item)
+                const FinishScope *f = &c.fin.scopes[x];
+                v = ld_agent(&f->word) & kScopeSumMask;
+                s = ld_agent(&f->parent);
+            }
+            acc.joins += 1;
+        }
+        // the freed slots onto the free list by ballot rank
+        const unsigned long long fm = __ballot(freeing);
+        if (fm) {
+            const uint32_t nf = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_fib_scopes.nfree);
+            if (freeing)
+                s_fib_scopes.freelist[nf + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u))] = slot;
+            s_fib_scopes.nfree = nf + (uint32_t)__popcll(fm);
+        }
+        const bool last = check_out_one(c, acc, s, v);
+        stamp(2, tst);
+        if (last) {
+            child[0] = kFibCont;
+            child[1] = s;
+            return 1;
+        }
+        return 0;
+    }
+
+    // the ring ran empty: the check-outs still in flight, to their ends
+    __device__ static void drain(const Ctx &c, Acc &acc, uint32_t *) {
+        if (c.defer) acc.joins += finish_drain(c.fin, acc.q, PassSum());
     }
 
     // an item leaving the wave names an HBM scope (its LDS scope promoted)
@@ -132,7 +241,13 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     HX_HIP(hipMalloc(&dmem, jb + 512));
     FibCtx ctx;
     ctx.n = n;
-    ctx.local = env_int("HCLIB_HIP_FIB_LOCAL", 0);  // LDS scopes: measured slower so far (profiles/r04/fib_stamps.log)
+    // LDS scopes (hx_finish.h LocalScopes, batched promotion): fib(30)
+    // 0.807 -> 0.688 ms (profiles/r04/fiblds_sweep.log)
+    ctx.local = env_int("HCLIB_HIP_FIB_LOCAL", 1);
+    ctx.defer = ctx.local && env_int("HCLIB_HIP_FIB_DEFER", 1);
+    // inline climb vs continuation items: 0.69-0.74 ms both, same box
+    // (profiles/r04/fibclimb_sweep.log); the inline walk runs fewer batches
+    ctx.climb = env_int("HCLIB_HIP_FIB_CLIMB", 1);
     ctx.fin.scopes = (FinishScope *)dmem;
     ctx.fin.next = (uint32_t *)((char *)dmem + ((jb + 255) & ~(size_t)255));
     ctx.fin.cap = (uint32_t)ids;

@@ -133,6 +133,52 @@ __device__ __forceinline__ uint32_t finish_check_out(const FinishArena &a, uint3
     return ran;
 }
 
+// finish_check_out split in two, so that an HBM check-out's round trip
+// overlaps other work: finish_issue starts the step on scope s (its atomic
+// and the {parent, cont} load), finish_resolve — called a batch later —
+// takes the result: not the last task out: done; the last: the continuation,
+// and the parent's step is issued in turn (root: the value is stored). One
+// step per lane in flight (q.s == kScopeRoot: none).
+struct FinishInFlight {
+    unsigned long long old = 0, pc = 0, v = 0;
+    uint32_t s = kScopeRoot;
+};
+
+__device__ __forceinline__ void finish_issue(const FinishArena &a, FinishInFlight &q, uint32_t s,
+                                             unsigned long long v) {
+    if (s >= a.cap) return;  // (never; see finish_check_out)
+    FinishScope *f = &a.scopes[s];
+    q.s = s;
+    q.v = v & kScopeSumMask;
+    q.pc = ld_agent((const unsigned long long *)&f->parent);
+    q.old = add_agent(&f->word, q.v - kScopeOne);
+}
+
+template <class Cont>
+__device__ __forceinline__ uint32_t finish_resolve(const FinishArena &a, FinishInFlight &q, Cont &&cont) {
+    if (q.s == kScopeRoot) return 0;
+    unsigned long long old = q.old, add = q.v;
+    if ((old & kScopeSumMask) + q.v > kScopeSumMask) {  // see finish_check_out (synchronous, rare)
+        old = add_agent(&a.scopes[q.s].word, (unsigned long long)0 - kScopeOne);
+        add = 0;
+    }
+    q.s = kScopeRoot;
+    if ((old >> 56) != 1) return 0;
+    const unsigned long long v = cont((uint32_t)(q.pc >> 32), (old + add) & kScopeSumMask) & kScopeSumMask;
+    const uint32_t p = (uint32_t)q.pc;
+    if (p == kScopeRoot) st_agent(a.root_value, v);
+    else finish_issue(a, q, p, v);
+    return 1;
+}
+
+// every step still in flight, to its end (before the wave goes idle)
+template <class Cont>
+__device__ __forceinline__ uint32_t finish_drain(const FinishArena &a, FinishInFlight &q, Cont &&cont) {
+    uint32_t ran = 0;
+    while (q.s != kScopeRoot) ran += finish_resolve(a, q, cont);
+    return ran;
+}
+
 // ------------------------------------------------ wave-local scopes (LDS)
 // Most scopes open and close inside one wave: its two (or k) tasks are pushed
 // onto the wave's own ring and popped by it again (LIFO), usually in the
@@ -279,38 +325,71 @@ __device__ __forceinline__ uint32_t finish_open_local(const FinishArena &a, Loca
 // unpromoted LDS slot). One LDS round trip per LDS step: the slot's meta
 // read is issued beside its atomic (a forwarded slot's word is dead, so the
 // stray add there is harmless).
+// With q (a free in-flight slot), the chain's first HBM step is issued into
+// it rather than waited for (finish_issue / finish_resolve). The walk runs
+// in lock step: per step one LDS atomic (its meta read beside it) per lane
+// still climbing; slots freed in a step go onto the free list by ballot rank
+// (no returning atomic), the list's length kept in a scalar until the end.
 template <int N, class Cont>
 __device__ __forceinline__ uint32_t finish_check_out_local(const FinishArena &a, LocalScopes<N> &ls, uint32_t s,
-                                                           unsigned long long value, Cont &&cont) {
+                                                           unsigned long long value, Cont &&cont,
+                                                           FinishInFlight *q = nullptr) {
     uint32_t ran = 0;
     unsigned long long v = value & kScopeSumMask;
-    while (s != kScopeRoot) {
-        if (!scope_is_lds(s)) return ran + finish_check_out(a, s, v, cont);
-        const uint32_t slot = s & (kScopeLds - 1);
-        if (slot >= (uint32_t)N) return ran;  // (never; see finish_check_out)
-        const hx_u32x4 meta = ls.meta[slot];
-        unsigned long long old = __hip_atomic_fetch_add(&ls.word[slot], v - kScopeOne, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_WORKGROUP),
-                           add = v;
-        if (meta.z) {  // promoted: the HBM copy counts from here on
-            s = meta.z - 1;
-            continue;
+    uint32_t nf = (uint32_t)__builtin_amdgcn_readfirstlane((int)ls.nfree);
+    bool go = true, hbm = false, freed_any = false;
+    while (__ballot(go)) {
+        bool freeing = false;
+        uint32_t slot = 0;
+        if (go) {
+            if (s == kScopeRoot) {
+                st_agent(a.root_value, v);
+                go = false;
+            } else if (!scope_is_lds(s)) {
+                hbm = true;
+                go = false;
+            } else {
+                slot = s & (kScopeLds - 1);
+                if (slot >= (uint32_t)N) {  // (never; see finish_check_out)
+                    go = false;
+                } else {
+                    const hx_u32x4 meta = ls.meta[slot];
+                    unsigned long long old = __hip_atomic_fetch_add(&ls.word[slot], v - kScopeOne, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_WORKGROUP),
+                                       add = v;
+                    if (meta.z) {
+                        s = meta.z - 1;  // promoted: the HBM copy counts from here on
+                    } else {
+                        if ((old & kScopeSumMask) + v > kScopeSumMask) {  // see finish_check_out
+                            old = __hip_atomic_fetch_add(&ls.word[slot], (unsigned long long)0 - kScopeOne,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            add = 0;
+                        }
+                        if ((old >> 56) != 1) {
+                            go = false;
+                        } else {
+                            freeing = true;
+                            v = cont(meta.y, (old + add) & kScopeSumMask) & kScopeSumMask;
+                            ++ran;
+                            s = meta.x;
+                        }
+                    }
+                }
+            }
         }
-        if ((old & kScopeSumMask) + v > kScopeSumMask) {  // see finish_check_out
-            old = __hip_atomic_fetch_add(&ls.word[slot], (unsigned long long)0 - kScopeOne, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-            add = 0;
-        }
-        if ((old >> 56) != 1) return ran;
-        const unsigned long long sum = (old + add) & kScopeSumMask;
-        // the slot is free again
-        const uint32_t pos = __hip_atomic_fetch_add(&ls.nfree, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        ls.freelist[pos] = slot;
-        v = cont(meta.y, sum) & kScopeSumMask;
-        ++ran;
-        s = meta.x;
+        const unsigned long long fm = __ballot(freeing);
+        if (freeing)
+            ls.freelist[nf + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u))] =
+                slot;
+        nf += (uint32_t)__popcll(fm);
+        freed_any = freed_any || fm != 0;
     }
-    st_agent(a.root_value, v);
+    if (freed_any) ls.nfree = nf;  // (every active lane: the same value)
+    asm volatile("" ::: "memory");
+    if (hbm) {
+        if (q && q->s == kScopeRoot) finish_issue(a, *q, s, v);
+        else ran += finish_check_out(a, s, v, cont);
+    }
     return ran;
 }
 

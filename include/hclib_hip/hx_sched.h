@@ -487,6 +487,19 @@ __device__ __forceinline__ void kind_export(const typename Kind::Ctx &ctx, uint3
     if constexpr (kind_has_export<Kind>::value) Kind::export_item(ctx, w, valid, err);
 }
 
+// Optional Kind hook: static void drain(const Ctx&, Acc&, uint32_t *err),
+// called by the whole wave when its ring runs empty, before the wave counts
+// itself idle: work the Kind left in flight across batches (fib's HBM
+// check-outs, hx_finish.h finish_issue) must end before termination can.
+template <class K, class = void>
+struct kind_has_drain : std::false_type {};
+template <class K>
+struct kind_has_drain<K, decltype((void)&K::drain)> : std::true_type {};
+template <class Kind>
+__device__ __forceinline__ void kind_drain(const typename Kind::Ctx &ctx, typename Kind::Acc &acc, uint32_t *err) {
+    if constexpr (kind_has_drain<Kind>::value) Kind::drain(ctx, acc, err);
+}
+
 // Try to publish `n` entries (ring positions bot..bot+n-1) as one chunk into
 // deque q. Called by the whole wave; returns true if the chunk is placed.
 // `occ`: the deque occupancy this wave saw at its last enqueue. While that
@@ -1491,6 +1504,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 busy_phase = false;
             }
             if (active) {
+                kind_drain<Kind>(ctx, acc, &g->err);
                 active = false;
                 wave_goes_idle<GLOBAL>(g, gv, pool);
                 tl.log(kTlIdle, 0);

@@ -250,6 +250,24 @@ def test_fib30_tasks_and_joins():
     assert st["joins"] == 1346269 - 1      # one finish scope per internal call
 
 
+@pytest.mark.parametrize("mode", [{"HCLIB_HIP_FIB_LOCAL": "0"},
+                                  {"HCLIB_HIP_FIB_CLIMB": "1", "HCLIB_HIP_FIB_DEFER": "0"},
+                                  {"HCLIB_HIP_FIB_CLIMB": "1", "HCLIB_HIP_FIB_DEFER": "1"},
+                                  {"HCLIB_HIP_FIB_CLIMB": "0", "HCLIB_HIP_FIB_DEFER": "0"},
+                                  {"HCLIB_HIP_FIB_CLIMB": "0", "HCLIB_HIP_FIB_DEFER": "1"}])
+def test_fib_finish_scope_modes(mode, monkeypatch):
+    """Every join mode gives the same value, tasks and joins: HBM scopes only;
+    LDS scopes (hx_finish.h LocalScopes) climbing inline or one level per task
+    (continuation items), with HBM check-outs waited for or resolved a batch
+    later (finish_issue / finish_resolve); fib(25) and fib(30)."""
+    for k, v in mode.items():
+        monkeypatch.setenv(k, v)
+    for n, want, calls in [(25, 75025, 242785), (30, 832040, 2692537)]:
+        v, st = H.fib(n)
+        assert v == want, (mode, n)
+        assert st["tasks"] == calls and st["joins"] == (calls - 1) // 2, (mode, n, st)
+
+
 # ------------------------------------------------------------------------ SW
 def _sw_inputs(size):
     a = open(os.path.join(GOLD, "sw", f"string1-{size}.txt"), "rb").read()
