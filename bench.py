@@ -634,9 +634,13 @@ def main():
         dscore, dagst = H.sw(s1, s2, 256, 256)
         del os.environ["HCLIB_HIP_SW_SCHED"]
         assert dscore == 128772
+        t1_rate = T1_GOLD[0] / (t1["kernel_ms"] * 1e-3)
         out["configs"] = {
-            "uts_t1_1gpu": {"nodes_per_s": T1_GOLD[0] / (t1["kernel_ms"] * 1e-3),
-                            "kernel_ms": t1["kernel_ms"]},
+            # roofline_frac: T1 against the same SHA-1 issue ceiling as
+            # roofline_uts (a 4.1 M-node tree: its launch ramp and drain show
+            # here)
+            "uts_t1_1gpu": {"nodes_per_s": t1_rate, "kernel_ms": t1["kernel_ms"],
+                            "roofline_frac": t1_rate / out["roofline_uts"]["peak"] if "roofline_uts" in out else None},
             "forasync_triad_2p28": {"GB_per_s": tri["gbs"], "ms": tri["ms"]},
             "fib30_gpu": {"tasks_per_s": fst["tasks"] / (fst["kernel_ms"] * 1e-3),
                           "tasks": fst["tasks"], "kernel_ms": fst["kernel_ms"]},

@@ -272,6 +272,10 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 1);
     HX_TRY(reset_sched(pool, 1, false, (uint32_t)grid));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
+    if (int rc0 = check_resident((const void *)k_fib, grid, 64, 0, "hclib_hip_fib")) {
+        (void)hipFree(dmem);
+        return rc0;
+    }
     hipLaunchKernelGGL(k_fib, dim3(grid), dim3(64), 0, m.stream, ctx, pool, m.globals, cfg);
     HX_HIP(hipGetLastError());
     HX_HIP(hipEventRecord(m.ev1, m.stream));

@@ -50,6 +50,10 @@ Module &mod();
 void set_error(const char *fmt, ...);
 int ensure_device();  // HCLIB_HIP_OK or HCLIB_HIP_ENODEV
 int hip_check(hipError_t e, const char *what);
+// A persistent launch (every worker waits for every other one to end) must
+// fit the chip at once: HCLIB_HIP_EINVAL, with the numbers, when `blocks`
+// workgroups of `threads` (and `lds` dynamic bytes) cannot all be resident
+int check_resident(const void *kern, int blocks, int threads, size_t lds, const char *what);
 // host -> device copy of `bytes` at `src` in `stream` order through a pinned
 // staging buffer: `src` may be freed as soon as the call returns
 int upload_async(void *dst, const void *src, size_t bytes, hipStream_t stream);

@@ -21,6 +21,19 @@ void set_error(const char *fmt, ...) {
     va_end(ap);
 }
 
+int check_resident(const void *kern, int blocks, int threads, size_t lds, const char *what) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess) return HCLIB_HIP_OK;
+    const long long cap = (long long)per_cu * mod().num_cus;
+    if (blocks > cap) {
+        set_error("%s: %d workgroups of %d threads cannot all be resident (%d per CU x %d CUs: LDS / registers); "
+                  "the persistent workers would wait on waves that never start (lower HCLIB_HIP_WAVES_PER_CU)",
+                  what, blocks, threads, per_cu, mod().num_cus);
+        return HCLIB_HIP_EINVAL;
+    }
+    return HCLIB_HIP_OK;
+}
+
 int hip_check(hipError_t e, const char *what) {
     if (e == hipSuccess) return HCLIB_HIP_OK;
     set_error("%s failed: %s", what, hipGetErrorString(e));

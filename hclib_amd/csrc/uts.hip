@@ -833,6 +833,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         if (wpg == 2) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 2> : k_uts_search<kUtsBin, 0, 1024, false, 2>;
         if (wpg == 4) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 4> : k_uts_search<kUtsBin, 0, 1024, false, 4>;
     }
+    HX_TRY(check_resident((const void *)kern, grid / wpg, 64 * wpg, 0, "hclib_hip_uts_search"));
     hipLaunchKernelGGL(kern, dim3(grid / wpg), dim3(64 * wpg), 0, m.stream, ctx, pool, m.globals, cfg);
     HX_HIP(hipGetLastError());
     HX_HIP(hipEventRecord(m.ev1, m.stream));

@@ -348,6 +348,11 @@ struct KindFixedChildren<K, decltype((void)K::kFixedChildren)> {
 };
 constexpr uint32_t kMaxChildren = 1u << 24;  // kend shares its descriptor word with delta
 
+// register carry through LDS (carry_lds) where the ring's stack has room;
+// HX_CARRY_LDS=0 builds keep carry_permute everywhere
+#ifndef HX_CARRY_LDS
+#define HX_CARRY_LDS 1
+#endif
 template <class Kind, int CAP>
 struct WaveStack {
     static constexpr int TW = Kind::kTmplWords;
@@ -362,6 +367,11 @@ struct WaveStack {
     // [0] busy cycles, [1] idle cycles, [2] spill cycles, [3] narrow-loop
     // cycles, [4] s_memtime at start, [5] s_memrealtime at start
     unsigned long long cyc[6];
+    // register carry's template slots (carry_lds: 2 x 16 B per spawning
+    // rank), on the 1,024-item rings only: the 512-item rings of the wide GEO
+    // trees run 8 waves per CU, whose stacks then just fit the 160 KiB
+    static constexpr bool kCarryLds = HX_CARRY_LDS && CAP >= 1024;
+    uint4 cscr[kCarryLds ? 128 : 1];
 };
 
 // lane 0 adds to a per-wave LDS sum (no return value, no wait)
@@ -839,6 +849,45 @@ __device__ __forceinline__ void carry_permute(unsigned long long spawn, uint32_t
     ck = lane - __umul24(r, mu);
 }
 
+// Register carry through LDS (WaveStack::kCarryLds; otherwise
+// carry_permute): every spawning lane stores its new task's template in slot
+// rank (its rank among the spawning lanes), output o reads slot o / mu and
+// is child o % mu of it. One LDS round trip where carry_permute takes three
+// dependent ones (ds_permute -> ds_bpermute -> 6 x ds_bpermute): the wave's
+// LDS operations complete in issue order, so the reads see the stores.
+template <int TW>
+__device__ __forceinline__ void carry_lds(uint4 *scr, unsigned long long spawn, uint32_t mu, const uint32_t *child,
+                                          uint32_t *ctmpl, uint32_t &ck, uint32_t rcp = 0) {
+    static_assert(TW == 2 || TW == 6, "templates are 2 or 6 words");
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(spawn >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
+    if ((spawn >> lane) & 1ull) {
+        if constexpr (TW == 6) {
+            scr[2 * rk] = make_uint4(child[0], child[1], child[2], child[3]);
+            *(uint2 *)&scr[2 * rk + 1] = make_uint2(child[4], child[5]);
+        } else {
+            *(uint2 *)&scr[2 * rk] = make_uint2(child[0], child[1]);
+        }
+    }
+    const uint32_t r = __umul24(lane, rcp ? rcp : rcp16(mu)) >> 16;  // lane / mu
+    if constexpr (TW == 6) {
+        const uint4 a = scr[2 * r];
+        const uint2 b = *(const uint2 *)&scr[2 * r + 1];
+        ctmpl[0] = a.x;
+        ctmpl[1] = a.y;
+        ctmpl[2] = a.z;
+        ctmpl[3] = a.w;
+        ctmpl[4] = b.x;
+        ctmpl[5] = b.y;
+    } else {
+        const uint2 a = *(const uint2 *)&scr[2 * r];
+        ctmpl[0] = a.x;
+        ctmpl[1] = a.y;
+    }
+    ck = lane - __umul24(r, mu);
+}
+
 // Uniform push: no lane has a residual range and every lane that spawned a
 // task spawned exactly `mu` (<= kPieces) children — every BIN-tree batch
 // after the root fan-out, every fib batch. Group starts are then
@@ -1053,7 +1102,8 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
             if (t2 <= (uint32_t)kWaveSize) {
                 // (a scalar walk over the spawn mask instead of the permute pair
                 // measured slower: T3L 31.8 -> 32.6 ms, profiles/r04/walk_ab.log)
-                carry_permute<TW>(sp2, mu2, n2, ch2, ns.ctmpl, ns.ck, rcp_fix);
+                if constexpr (WaveStack<Kind, CAP>::kCarryLds) carry_lds<TW>(st.cscr, sp2, mu2, ch2, ns.ctmpl, ns.ck, rcp_fix);
+                else carry_permute<TW>(sp2, mu2, n2, ch2, ns.ctmpl, ns.ck, rcp_fix);
                 carry = t2;
                 continue;
             }
@@ -1842,7 +1892,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             const uint32_t hungry0 = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
             if (cfg.carry && uniform && tout > 0 && tout <= (uint32_t)kWaveSize &&
                 !(hungry0 > 0 && (top - bot) + tout >= spill_lo_now(cfg, hungry0))) {
-                carry_permute<TW>(spawn, mu, nch, child, ctmpl, ck);
+                if constexpr (WaveStack<Kind, CAP>::kCarryLds) carry_lds<TW>(st.cscr, spawn, mu, child, ctmpl, ck);
+                else carry_permute<TW>(spawn, mu, nch, child, ctmpl, ck);
                 carry = tout;
                 if (HX_STAMPS && cfg.stamps) cyc_push += __builtin_amdgcn_s_memtime() - ts0;
                 if (HX_STAMPS && cfg.stamps) t_batch = __builtin_amdgcn_s_memtime();

@@ -250,6 +250,17 @@ def test_fib30_tasks_and_joins():
     assert st["joins"] == 1346269 - 1      # one finish scope per internal call
 
 
+def test_persistent_launch_that_cannot_be_resident_fails_fast(monkeypatch):
+    """A megakernel grid the CUs cannot hold at once (here 64 fib waves per CU
+    against ~5 that fit its LDS) is refused on the host before the launch,
+    instead of spinning to the idle timeout on waves that never start."""
+    monkeypatch.setenv("HCLIB_HIP_WAVES_PER_CU", "64")
+    with pytest.raises(H.HclibError, match="cannot all be resident"):
+        H.fib(20)
+    monkeypatch.delenv("HCLIB_HIP_WAVES_PER_CU")
+    assert H.fib(20)[0] == 6765
+
+
 @pytest.mark.parametrize("mode", [{"HCLIB_HIP_FIB_LOCAL": "0"},
                                   {"HCLIB_HIP_FIB_CLIMB": "1", "HCLIB_HIP_FIB_DEFER": "0"},
                                   {"HCLIB_HIP_FIB_CLIMB": "1", "HCLIB_HIP_FIB_DEFER": "1"},
