@@ -747,7 +747,10 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     const int ring_used = geo_fixed && !(nshards > 1 || max_levels > 0) ? env_int("HCLIB_HIP_UTS_RING", ring_default) : 512;
     // sharded launches of a rank attached to a global region share work
     const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
-    int spill_lo_default = bin ? 72 : (geo_fixed && ring_used < 512) ? 128 : 224;
+    // BIN trees: 66 since the register carry went through LDS (T3L 30.64 ->
+    // 30.20 ms same-box against 72, profiles/r04/sc_ab_t3l*.log, t3l3_spill.log);
+    // it must stay above one batch (64) or the narrow loop never runs
+    int spill_lo_default = bin ? 66 : (geo_fixed && ring_used < 512) ? 128 : 224;
     // seeded fixed-shape trees (below) start with every wave busy, so a wave
     // keeps more before it feeds others: T1 0.285 -> 0.248 ms at 336, T1L
     // 2.70 -> 2.38, T1XL's 8-way shards 4.94 -> 4.75 at 448
