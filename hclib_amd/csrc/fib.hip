@@ -29,7 +29,10 @@ struct FibCtx {
 };
 
 // the wave's LDS finish scopes (file scope: every access is a ds_* op)
-constexpr int kFibLocalScopes = 512;
+#ifndef HX_FIB_SCOPES
+#define HX_FIB_SCOPES 512
+#endif
+constexpr int kFibLocalScopes = HX_FIB_SCOPES;
 __shared__ LocalScopes<kFibLocalScopes> s_fib_scopes;
 // the wave's block of HBM scope ids (hx_finish.h finish_open `blk`)
 __shared__ uint32_t s_fib_blk[2];
@@ -41,6 +44,9 @@ struct FibKind {
     static constexpr int kWords = 4;
     static constexpr bool kPure = false;           // scopes are opened / checked out in HBM
     static constexpr bool kBoundedChildren = true;  // 0, 1 (a continuation item) or 2
+#ifdef HX_FIB_PIECES
+    static constexpr int kPieces = HX_FIB_PIECES;  // (small-ring builds: a lane's batch output bound)
+#endif
     using Ctx = FibCtx;
     struct Acc {
         unsigned long long tasks = 0, joins = 0;
@@ -52,8 +58,8 @@ struct FibKind {
             c[0] = wave_sum(tasks);
             c[1] = wave_sum(joins);
 #if defined(HX_STAMPS) && HX_STAMPS
-            c[2] = wave_sum(cyc[0] + cyc[1]);  // (the scheduler keeps c[4..7])
-            c[3] = wave_sum(cyc[2]);
+            c[2] = wave_sum(cyc[1]);  // check-outs entered with the in-flight slot free
+            c[3] = wave_sum(cyc[2]);  // ... with it busy (an HBM step there waits)  (the scheduler keeps c[4..7])
 #endif
         }
     };
@@ -131,10 +137,12 @@ struct FibKind {
             return 2;
         }
         if (!c.local || c.climb) {  // a leaf returns n: check out, continuations inline
+            const bool busy = acc.q.s != kScopeRoot;
+            stamp(-1, tst);
             acc.joins += c.local ? finish_check_out_local(c.fin, s_fib_scopes, t[1], (unsigned long long)n, PassSum(),
                                                           c.defer ? &acc.q : nullptr)
                                  : finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
-            stamp(2, tst);
+            stamp(busy ? 2 : 1, tst);
             return 0;
         }
         // a leaf checks n out of its scope; a continuation item frees its
@@ -193,7 +201,10 @@ struct FibKind {
     }
 };
 
-constexpr int kFibCap = 1024;  // ring items per wave (16 KiB of LDS)
+#ifndef HX_FIB_CAP
+#define HX_FIB_CAP 1024
+#endif
+constexpr int kFibCap = HX_FIB_CAP;  // ring items per wave (16 KiB of LDS at 1,024)
 
 __global__ __launch_bounds__(64) void k_fib(FibCtx ctx, PoolView pool, SchedGlobals *g,
                                             SchedConfig cfg) {
