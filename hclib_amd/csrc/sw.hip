@@ -1894,6 +1894,39 @@ __device__ bool sw_pk2_tile(const SwCtx &c, const SwPkTile &T, int *top, int *to
     return true;
 }
 
+// The score wave, after staging the right neighbour (tile t + 1): poll its
+// top row (the up-right tile's bottom row) into LDS while this tile's sweep
+// runs (misc + kSwPkMisc + 256, then misc[8] = t + 1), so a kept neighbour
+// starts without a global load. Gives up once this tile is done (misc[4]):
+// the next tile then loads the row itself.
+__device__ __forceinline__ void sw_pk_prefetch_top(const SwCtx &c, uint32_t t, int *misc) {
+    int *ntop = misc + kSwPkMisc + 256;
+    const sw_gran *src = c.gbot + (size_t)(t + 1 - (uint32_t)c.ntw) * c.tw;
+    const int xmax = c.tw - 1;
+    for (uint32_t n = 0;; ++n) {
+        sw_gran g[kSwPkMaxTw / 64];
+        bool ready = true;
+#pragma unroll
+        for (int k = 0; k < kSwPkMaxTw / 64; ++k) {
+            const int x = lane_id() + 64 * k;
+            g[k] = k * 64 < c.tw ? ld_agent(&src[x < c.tw ? x : xmax]) : (1ull << 32);
+        }
+#pragma unroll
+        for (int k = 0; k < kSwPkMaxTw / 64; ++k) ready = ready && (g[k] >> 32) == 1ull;
+        if (__ballot(!ready) == 0) {
+#pragma unroll
+            for (int k = 0; k < kSwPkMaxTw / 64; ++k) {
+                const int x = lane_id() + 64 * k;
+                if (x < c.tw) ntop[x] = (int)(uint32_t)g[k];
+            }
+            if (lane_id() == 0) lds_flag_st(&misc[8], (int)t + 1);
+            return;
+        }
+        if (lds_flag_ld(&misc[4]) == (int)t + 1) return;
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
 // The promise DAG with the packed body: workgroups of three waves, wave 0
 // the sweep (and the tickets), wave 1 the scores, wave 2 run_dag_group's
 // helper (waiter prefetch, datums: its global round trips stay off the
@@ -1951,34 +1984,7 @@ struct SwDagPkKind {
             // starts without a global load
             // (after the sweep wave has read this tile's own LDS top row: it
             // consumes chunk 0 only after that)
-            if (next && i > 0 && sw_pk_wait(c, &misc[6], 1)) {
-                int *ntop = misc + kSwPkMisc + 256;
-                const sw_gran *src = c.gbot + (size_t)(t + 1 - (uint32_t)c.ntw) * c.tw;
-                const int xmax = c.tw - 1;
-                for (uint32_t n = 0;; ++n) {
-                    sw_gran g[kSwPkMaxTw / 64];
-                    bool ready = true;
-#pragma unroll
-                    for (int k = 0; k < kSwPkMaxTw / 64; ++k) {
-                        const int x = lane_id() + 64 * k;
-                        g[k] = k * 64 < c.tw ? ld_agent(&src[x < c.tw ? x : xmax]) : (1ull << 32);
-                    }
-#pragma unroll
-                    for (int k = 0; k < kSwPkMaxTw / 64; ++k) ready = ready && (g[k] >> 32) == 1ull;
-                    if (__ballot(!ready) == 0) {
-#pragma unroll
-                        for (int k = 0; k < kSwPkMaxTw / 64; ++k) {
-                            const int x = lane_id() + 64 * k;
-                            if (x < c.tw) ntop[x] = (int)(uint32_t)g[k];
-                        }
-                        if (lane_id() == 0) lds_flag_st(&misc[8], (int)t + 1);
-                        break;
-                    }
-                    // give up once this tile's sweep is done (the next one loads it)
-                    if (lds_flag_ld(&misc[4]) == (int)t + 1) break;
-                    __builtin_amdgcn_s_sleep(8);
-                }
-            }
+            if (next && i > 0 && sw_pk_wait(c, &misc[6], 1)) sw_pk_prefetch_top(c, t, misc);
             return true;
         }
         const bool from_lds = j > 0 && misc[0] == (int)t - 1;
@@ -2084,33 +2090,7 @@ struct SwDagPk2Kind {
             if (lane_id() == 0) misc[7] = next ? (int)t + 1 : -1;
             // the right neighbour's top row into LDS (as SwDagPkKind), once A
             // has taken this tile's
-            if (next && i > 0 && sw_pk_wait(c, &misc[6], 1)) {
-                int *ntop = misc + kSwPkMisc + 256;
-                const sw_gran *src = c.gbot + (size_t)(t + 1 - (uint32_t)c.ntw) * c.tw;
-                const int xmax = c.tw - 1;
-                for (uint32_t n = 0;; ++n) {
-                    sw_gran g[kSwPkMaxTw / 64];
-                    bool ready = true;
-#pragma unroll
-                    for (int k = 0; k < kSwPkMaxTw / 64; ++k) {
-                        const int x = lane_id() + 64 * k;
-                        g[k] = k * 64 < c.tw ? ld_agent(&src[x < c.tw ? x : xmax]) : (1ull << 32);
-                    }
-#pragma unroll
-                    for (int k = 0; k < kSwPkMaxTw / 64; ++k) ready = ready && (g[k] >> 32) == 1ull;
-                    if (__ballot(!ready) == 0) {
-#pragma unroll
-                        for (int k = 0; k < kSwPkMaxTw / 64; ++k) {
-                            const int x = lane_id() + 64 * k;
-                            if (x < c.tw) ntop[x] = (int)(uint32_t)g[k];
-                        }
-                        if (lane_id() == 0) lds_flag_st(&misc[8], (int)t + 1);
-                        break;
-                    }
-                    if (lds_flag_ld(&misc[4]) == (int)t + 1) break;
-                    __builtin_amdgcn_s_sleep(8);
-                }
-            }
+            if (next && i > 0 && sw_pk_wait(c, &misc[6], 1)) sw_pk_prefetch_top(c, t, misc);
             return true;
         }
         const bool from_lds = j > 0 && misc[0] == (int)t - 1;

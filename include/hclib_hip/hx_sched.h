@@ -353,6 +353,9 @@ constexpr uint32_t kMaxChildren = 1u << 24;  // kend shares its descriptor word 
 #ifndef HX_CARRY_LDS
 #define HX_CARRY_LDS 1
 #endif
+#ifndef HX_CARRY_HOIST
+#define HX_CARRY_HOIST 1  // the narrow loop's carry slots precomputed (narrow_loop r_fix)
+#endif
 template <class Kind, int CAP>
 struct WaveStack {
     static constexpr int TW = Kind::kTmplWords;
@@ -855,6 +858,37 @@ __device__ __forceinline__ void carry_permute(unsigned long long spawn, uint32_t
 // is child o % mu of it. One LDS round trip where carry_permute takes three
 // dependent ones (ds_permute -> ds_bpermute -> 6 x ds_bpermute): the wave's
 // LDS operations complete in issue order, so the reads see the stores.
+// The store side, and the read of slot r (this lane's source rank).
+template <int TW>
+__device__ __forceinline__ void carry_lds_slot(uint4 *scr, unsigned long long spawn, const uint32_t *child,
+                                               uint32_t *ctmpl, uint32_t r) {
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(spawn >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
+    if ((spawn >> lane) & 1ull) {
+        if constexpr (TW == 6) {
+            scr[2 * rk] = make_uint4(child[0], child[1], child[2], child[3]);
+            *(uint2 *)&scr[2 * rk + 1] = make_uint2(child[4], child[5]);
+        } else {
+            *(uint2 *)&scr[2 * rk] = make_uint2(child[0], child[1]);
+        }
+    }
+    if constexpr (TW == 6) {
+        const uint4 a = scr[2 * r];
+        const uint2 b = *(const uint2 *)&scr[2 * r + 1];
+        ctmpl[0] = a.x;
+        ctmpl[1] = a.y;
+        ctmpl[2] = a.z;
+        ctmpl[3] = a.w;
+        ctmpl[4] = b.x;
+        ctmpl[5] = b.y;
+    } else {
+        const uint2 a = *(const uint2 *)&scr[2 * r];
+        ctmpl[0] = a.x;
+        ctmpl[1] = a.y;
+    }
+}
+
 template <int TW>
 __device__ __forceinline__ void carry_lds(uint4 *scr, unsigned long long spawn, uint32_t mu, const uint32_t *child,
                                           uint32_t *ctmpl, uint32_t &ck, uint32_t rcp = 0) {
@@ -1065,6 +1099,10 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
         if (mu_fix > (uint32_t)kPieces) mu_fix = 0;
         rcp_fix = mu_fix ? rcp16(mu_fix) : 0u;
     }
+    // ... and so are each lane's carry source slot and child index
+    const bool hoist = HX_CARRY_HOIST && mu_fix != 0;  // (wave-uniform)
+    const uint32_t r_fix = hoist ? __umul24(lane, rcp_fix) >> 16 : 0u;
+    const uint32_t ck_fix = hoist ? lane - __umul24(r_fix, mu_fix) : 0u;
     while (true) {
         const bool h = lane < carry;
         uint32_t ch2[TW];
@@ -1102,7 +1140,14 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
             if (t2 <= (uint32_t)kWaveSize) {
                 // (a scalar walk over the spawn mask instead of the permute pair
                 // measured slower: T3L 31.8 -> 32.6 ms, profiles/r04/walk_ab.log)
-                if constexpr (WaveStack<Kind, CAP>::kCarryLds) carry_lds<TW>(st.cscr, sp2, mu2, ch2, ns.ctmpl, ns.ck, rcp_fix);
+                if constexpr (WaveStack<Kind, CAP>::kCarryLds) {
+                    if (hoist) {
+                        carry_lds_slot<TW>(st.cscr, sp2, ch2, ns.ctmpl, r_fix);
+                        ns.ck = ck_fix;
+                    } else {
+                        carry_lds<TW>(st.cscr, sp2, mu2, ch2, ns.ctmpl, ns.ck, rcp_fix);
+                    }
+                }
                 else carry_permute<TW>(sp2, mu2, n2, ch2, ns.ctmpl, ns.ck, rcp_fix);
                 carry = t2;
                 continue;
