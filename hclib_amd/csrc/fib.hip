@@ -58,8 +58,8 @@ struct FibKind {
             c[0] = wave_sum(tasks);
             c[1] = wave_sum(joins);
 #if defined(HX_STAMPS) && HX_STAMPS
-            c[2] = wave_sum(cyc[1]);  // check-outs entered with the in-flight slot free
-            c[3] = wave_sum(cyc[2]);  // ... with it busy (an HBM step there waits)  (the scheduler keeps c[4..7])
+            c[2] = wave_sum(cyc[1]);  // check-out cycles
+            c[3] = wave_sum(cyc[2]);  // lock-step climb iterations  (the scheduler keeps c[4..7])
 #endif
         }
     };
@@ -139,10 +139,20 @@ struct FibKind {
         if (!c.local || c.climb) {  // a leaf returns n: check out, continuations inline
             const bool busy = acc.q.s != kScopeRoot;
             stamp(-1, tst);
+#if defined(HX_STAMPS) && HX_STAMPS
+            uint32_t steps = 0;
+            uint32_t *stp = lead ? &steps : nullptr;
+#else
+            uint32_t *stp = nullptr;
+#endif
             acc.joins += c.local ? finish_check_out_local(c.fin, s_fib_scopes, t[1], (unsigned long long)n, PassSum(),
-                                                          c.defer ? &acc.q : nullptr)
+                                                          c.defer ? &acc.q : nullptr, stp)
                                  : finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
-            stamp(busy ? 2 : 1, tst);
+            stamp(1, tst);
+#if defined(HX_STAMPS) && HX_STAMPS
+            acc.cyc[2] += steps;  // (c[3]: lock-step iterations, first active lane)
+#endif
+            (void)busy;
             return 0;
         }
         // a leaf checks n out of its scope; a continuation item frees its

@@ -333,12 +333,13 @@ __device__ __forceinline__ uint32_t finish_open_local(const FinishArena &a, Loca
 template <int N, class Cont>
 __device__ __forceinline__ uint32_t finish_check_out_local(const FinishArena &a, LocalScopes<N> &ls, uint32_t s,
                                                            unsigned long long value, Cont &&cont,
-                                                           FinishInFlight *q = nullptr) {
+                                                           FinishInFlight *q = nullptr, uint32_t *steps = nullptr) {
     uint32_t ran = 0;
     unsigned long long v = value & kScopeSumMask;
     uint32_t nf = (uint32_t)__builtin_amdgcn_readfirstlane((int)ls.nfree);
     bool go = true, hbm = false, freed_any = false;
     while (__ballot(go)) {
+        if (steps) ++*steps;  // (diagnostics: lock-step iterations)
         bool freeing = false;
         uint32_t slot = 0;
         if (go) {

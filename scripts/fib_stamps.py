@@ -16,5 +16,5 @@ for local in ("0", "1"):
     nb = max(1, c[13])
     print(f"fib30 local={local}: ms={st['kernel_ms']:.3f} batches={nb} tasks/batch={st['tasks'] / nb:.1f} "
           f"cycles/batch form={c[7] / nb:.0f} process={c[8] / nb:.0f} push={c[4] / nb:.0f} busy={c[9] / nb:.0f} "
-          f"spill={c[11] / nb:.0f} busy_frac={st['busy_frac']:.2f} | check-out cycles/batch: slot free at entry={c[2] / nb:.0f} "
-          f"slot busy={c[3] / nb:.0f}", flush=True)
+          f"spill={c[11] / nb:.0f} busy_frac={st['busy_frac']:.2f} | check-out cycles/batch={c[2] / nb:.0f} "
+          f"climb iterations/batch={c[3] / nb:.2f}", flush=True)
