@@ -23,7 +23,7 @@ struct FibCtx {
     int n;
     int local;  // scopes in the wave's LDS while they stay inside it (hx_finish.h LocalScopes)
     int defer;  // HBM check-out steps issued in one batch, resolved in the next (finish_issue)
-    int climb;  // LDS mode: a leaf climbs its scope chain inline (else one level per task: kFibCont items)
+    int climb;  // LDS mode: scopes a leaf completes inline (then, or with 0 at once, kFibCont items)
     int blocks; // HBM scope ids taken kScopeBlock at a time per wave
     FinishArena fin;
 };
@@ -120,7 +120,7 @@ struct FibKind {
         // the HBM check-out this lane issued a batch ago: its result is in
         if (c.defer) acc.joins += finish_resolve(c.fin, acc.q, PassSum());
         stamp(0, tst);
-        const bool cont_item = c.local && !c.climb && t[0] == kFibCont;
+        const bool cont_item = c.local && t[0] == kFibCont;
         const int n = cont_item ? 0 : (int)t[0] - 1 - (int)k;
         const bool spawn = !cont_item && n >= 2;
         if (!cont_item) acc.tasks += 1;
@@ -136,7 +136,7 @@ struct FibKind {
             child[1] = j;
             return 2;
         }
-        if (!c.local || c.climb) {  // a leaf returns n: check out, continuations inline
+        if (!c.local || (c.climb && !cont_item)) {  // a leaf returns n: check out, continuations inline
             const bool busy = acc.q.s != kScopeRoot;
             stamp(-1, tst);
 #if defined(HX_STAMPS) && HX_STAMPS
@@ -145,14 +145,20 @@ struct FibKind {
 #else
             uint32_t *stp = nullptr;
 #endif
+            uint32_t pend = kScopeRoot;  // a completed scope past c.climb levels: continued as an item
             acc.joins += c.local ? finish_check_out_local(c.fin, s_fib_scopes, t[1], (unsigned long long)n, PassSum(),
-                                                          c.defer ? &acc.q : nullptr, stp)
+                                                          c.defer ? &acc.q : nullptr, stp, (uint32_t)c.climb, &pend)
                                  : finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
             stamp(1, tst);
 #if defined(HX_STAMPS) && HX_STAMPS
             acc.cyc[2] += steps;  // (c[3]: lock-step iterations, first active lane)
 #endif
             (void)busy;
+            if (pend != kScopeRoot) {
+                child[0] = kFibCont;
+                child[1] = pend;
+                return 1;
+            }
             return 0;
         }
         // a leaf checks n out of its scope; a continuation item frees its
@@ -266,9 +272,11 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     // 0.807 -> 0.688 ms (profiles/r04/fiblds_sweep.log)
     ctx.local = env_int("HCLIB_HIP_FIB_LOCAL", 1);
     ctx.defer = ctx.local && env_int("HCLIB_HIP_FIB_DEFER", 1);
-    // inline climb vs continuation items: 0.69-0.74 ms both, same box
+    // LDS scopes a leaf's check-out completes inline before it hands the
+    // climb on as a continuation item (0: one level per task, every climb an
+    // item). Inline vs items: 0.69-0.74 ms both, same box
     // (profiles/r04/fibclimb_sweep.log); the inline walk runs fewer batches
-    ctx.climb = env_int("HCLIB_HIP_FIB_CLIMB", 1);
+    ctx.climb = env_int("HCLIB_HIP_FIB_CLIMB", 1 << 30);
     ctx.fin.scopes = (FinishScope *)dmem;
     ctx.fin.next = (uint32_t *)((char *)dmem + ((jb + 255) & ~(size_t)255));
     ctx.fin.cap = (uint32_t)ids;
