@@ -86,9 +86,10 @@ struct FibKind {
         if (scope_is_lds(s)) {
             const uint32_t slot = s & (kScopeLds - 1);
             if (slot >= (uint32_t)kFibLocalScopes) return false;  // (never)
-            const hx_u32x4 meta = s_fib_scopes.meta[slot];
+            // the atomic first, the record read behind it (one round trip)
             unsigned long long old = __hip_atomic_fetch_add(&s_fib_scopes.word[slot], v - kScopeOne, __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+            const hx_u32x4 meta = s_fib_scopes.meta[slot];
             if (!meta.z) {
                 if ((old & kScopeSumMask) + v > kScopeSumMask)  // see finish_check_out
                     old = __hip_atomic_fetch_add(&s_fib_scopes.word[slot], (unsigned long long)0 - kScopeOne,

@@ -357,10 +357,14 @@ __device__ __forceinline__ uint32_t finish_check_out_local(const FinishArena &a,
                 if (slot >= (uint32_t)N) {  // (never; see finish_check_out)
                     go = false;
                 } else {
-                    const hx_u32x4 meta = ls.meta[slot];
-                    unsigned long long old = __hip_atomic_fetch_add(&ls.word[slot], v - kScopeOne, __ATOMIC_RELAXED,
+                    // the atomic first, the record read behind it: both in
+                    // flight together (one round trip per step)
+                    unsigned long long *wp = &ls.word[slot];
+                    const hx_u32x4 *mp = &ls.meta[slot];
+                    unsigned long long old = __hip_atomic_fetch_add(wp, v - kScopeOne, __ATOMIC_RELAXED,
                                                                     __HIP_MEMORY_SCOPE_WORKGROUP),
                                        add = v;
+                    const hx_u32x4 meta = *mp;
                     if (meta.z) {
                         s = meta.z - 1;  // promoted: the HBM copy counts from here on
                     } else {
