@@ -299,6 +299,11 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_FIB_HUNGER", 8);
+    // ramp-up / tail (more than 1/8 of the waves hungry): spill threshold,
+    // chunk size and hunger-read interval then (0: the steady-state values)
+    cfg.spill_lo_hungry = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO_HUNGRY", 0);
+    cfg.ramp_chunk = (uint32_t)env_int("HCLIB_HIP_FIB_RAMP_CHUNK", 0);
+    cfg.hunger_fast = (uint32_t)env_int("HCLIB_HIP_FIB_HUNGER_FAST", 0);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 1);
     HX_TRY(reset_sched(pool, 1, false, (uint32_t)grid));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
