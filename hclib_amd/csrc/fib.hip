@@ -25,6 +25,8 @@ struct FibCtx {
     int defer;  // HBM check-out steps issued in one batch, resolved in the next (finish_issue)
     int climb;  // LDS mode: scopes a leaf completes inline (then, or with 0 at once, kFibCont items)
     int blocks; // HBM scope ids taken kScopeBlock at a time per wave
+    uint32_t *seed;     // breadth-first seeding (HCLIB_HIP_FIB_SEED): [0] ready flag, [1] items, [64..] items; or null
+    int seed_per_wave;  // ... items per worker it aims at
     FinishArena fin;
 };
 
@@ -36,6 +38,9 @@ constexpr int kFibLocalScopes = HX_FIB_SCOPES;
 __shared__ LocalScopes<kFibLocalScopes> s_fib_scopes;
 // the wave's block of HBM scope ids (hx_finish.h finish_open `blk`)
 __shared__ uint32_t s_fib_blk[2];
+// items a seeding level may hold (worker 0 expands the levels in its own,
+// still empty, ring arrays: d[] and t1[], one {n, parent scope} per slot)
+constexpr uint32_t kFibSeedCap = 1024;
 
 struct FibKind {
     // template = {n + 1 of the parent call, the parent's scope}; child k is
@@ -205,6 +210,88 @@ struct FibKind {
         return 0;
     }
 
+    // Breadth-first seeding: worker 0 runs the call tree's top levels (each
+    // internal call opens an HBM scope, the calls below it are the next
+    // level) until the next level would pass workers x seed_per_wave items,
+    // publishes the last level, and every worker takes an equal share as
+    // its first ring items — all waves busy from the start instead of
+    // waiting for the work to spread from one root.
+    __device__ static bool seeding(const Ctx &c) { return c.seed != nullptr; }
+    template <class WS>
+    __device__ static uint32_t seed(const Ctx &c, Acc &acc, WS &st, uint32_t gid, uint32_t nwaves, uint32_t spin_ms,
+                                    uint32_t *err) {
+        const uint32_t lane = (uint32_t)lane_id();
+        uint32_t *flag = c.seed, *items = c.seed + 64;
+        if (gid == 0) {
+            static_assert(sizeof(st.d) / sizeof(st.d[0]) >= kFibSeedCap && sizeof(st.t1) / sizeof(st.t1[0]) >= kFibSeedCap,
+                          "the seeding levels live in the ring arrays");
+            unsigned long long tgt = (unsigned long long)nwaves * (unsigned long long)c.seed_per_wave;
+            const uint32_t target = tgt > kFibSeedCap ? kFibSeedCap : (uint32_t)tgt;
+            uint32_t *cur = (uint32_t *)st.d, *nxt = (uint32_t *)st.t1;
+            if (lane == 0) {
+                cur[0] = (uint32_t)c.n;
+                cur[1] = kScopeRoot;
+            }
+            uint32_t cnt = 1;
+            while (cnt > 0 && 2 * cnt <= target) {
+                uint32_t ncnt = 0;
+                for (uint32_t b = 0; b < cnt; b += 64) {
+                    const uint32_t i = b + lane;
+                    const bool has = i < cnt;
+                    const uint32_t m = has ? cur[2 * i] : 0u, p = has ? cur[2 * i + 1] : kScopeRoot;
+                    const bool open = has && m >= 2;
+                    const uint32_t S = finish_open(c.fin, open, p, 2, 0, err, c.blocks ? s_fib_blk : nullptr);
+                    const unsigned long long om = __ballot(open);
+                    const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32),
+                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u));
+                    if (open) {
+                        const uint32_t o = ncnt + 2 * rk;
+                        nxt[2 * o] = m - 1;
+                        nxt[2 * o + 1] = S;
+                        nxt[2 * o + 2] = m - 2;
+                        nxt[2 * o + 3] = S;
+                    }
+                    if (has) acc.tasks += 1;
+                    if (has && !open) acc.joins += finish_check_out(c.fin, p, (unsigned long long)m, PassSum());
+                    ncnt += 2u * (uint32_t)__popcll(om);
+                }
+                uint32_t *t = cur;
+                cur = nxt;
+                nxt = t;
+                cnt = ncnt;
+            }
+            for (uint32_t i = lane; i < cnt; i += 64) {
+                st_agent(&items[2 * i], cur[2 * i]);
+                st_agent(&items[2 * i + 1], cur[2 * i + 1]);
+            }
+            if (lane == 0) st_agent(&flag[1], cnt);
+            release_agent();
+            if (lane == 0) st_agent(&flag[0], 1u);
+        }
+        uint32_t ready = 0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (true) {
+            if (lane == 0) ready = ld_agent(&flag[0]);
+            ready = (uint32_t)__builtin_amdgcn_readfirstlane((int)ready);
+            if (ready) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * spin_ms) {
+                if (lane == 0) dev_error(err, kErrSpinTimeout);
+                return 0;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        acquire_agent();
+        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_agent(&flag[1]));
+        const uint32_t lo = (uint32_t)(((unsigned long long)cnt * gid) / nwaves),
+                       hi = (uint32_t)(((unsigned long long)cnt * (gid + 1)) / nwaves);
+        for (uint32_t j = lane; j < hi - lo; j += 64) {
+            const uint32_t tm[2] = {ld_agent(&items[2 * (lo + j)]) + 1u, ld_agent(&items[2 * (lo + j) + 1])};
+            store_tmpl(st, j, tm);  // template {n + 1, scope}: child 0 is the call fib(n)
+            st.d[j] = make_uint2(0u, 1u);
+        }
+        return hi - lo;
+    }
+
     // the ring ran empty: the check-outs still in flight, to their ends
     __device__ static void drain(const Ctx &c, Acc &acc, uint32_t *) {
         if (c.defer) acc.joins += finish_drain(c.fin, acc.q, PassSum());
@@ -255,8 +342,10 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
         set_error("hclib_hip_fib: n too large for the join arena");
         return HCLIB_HIP_EINVAL;
     }
+    // 3 waves per CU with seeding (fib(30) 0.65 -> 0.48-0.49 ms against 2,
+    // profiles/r04/fibseed2_sweep.log)
     const int grid = env_int("HCLIB_HIP_GRID", 0) > 0 ? env_int("HCLIB_HIP_GRID", 0)
-                                                    : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 2);
+                                                    : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 3);
     const int blocks = env_int("HCLIB_HIP_FIB_BLOCKS", 1);
     // the arena: every scope once, plus each wave's last partly used id block
     const unsigned long long ids = scopes + 1 + (blocks ? (unsigned long long)grid * kScopeBlock : 0ull);
@@ -265,8 +354,13 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
         return HCLIB_HIP_EINVAL;
     }
     const size_t jb = sizeof(FinishScope) * (size_t)ids;
+    // seeding buffer behind the arena's counters: [0] flag, [1] count, [64..] items
+    // (2 items per worker, at most kFibSeedCap: fib(30) 0.70-0.74 -> 0.47-0.49 ms,
+    // profiles/r04/fibseed_sweep.log, fibseed2_sweep.log; 0: from one root)
+    const int seed_pw = env_int("HCLIB_HIP_FIB_SEED", 2);
+    const size_t sb = seed_pw > 0 ? (64 + 2 * (size_t)kFibSeedCap) * 4 : 0;
     void *dmem = nullptr;
-    HX_HIP(hipMalloc(&dmem, jb + 512));
+    HX_HIP(hipMalloc(&dmem, jb + 512 + sb));
     FibCtx ctx;
     ctx.n = n;
     // LDS scopes (hx_finish.h LocalScopes, batched promotion): fib(30)
@@ -284,6 +378,12 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     ctx.blocks = blocks;
     ctx.fin.root_value = (unsigned long long *)(ctx.fin.next + 16);
     HX_HIP(hipMemsetAsync(ctx.fin.next, 0, 256, m.stream));
+    ctx.seed = nullptr;
+    ctx.seed_per_wave = seed_pw;
+    if (seed_pw > 0) {
+        ctx.seed = (uint32_t *)((char *)dmem + ((jb + 255) & ~(size_t)255) + 256);
+        HX_HIP(hipMemsetAsync(ctx.seed, 0, 256, m.stream));
+    }
     PoolView pool;
     HX_TRY(make_pool((uint32_t)env_int("HCLIB_HIP_DEQUES", 64),
                      (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
@@ -305,7 +405,8 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     cfg.ramp_chunk = (uint32_t)env_int("HCLIB_HIP_FIB_RAMP_CHUNK", 0);
     cfg.hunger_fast = (uint32_t)env_int("HCLIB_HIP_FIB_HUNGER_FAST", 0);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 1);
-    HX_TRY(reset_sched(pool, 1, false, (uint32_t)grid));
+    // seeded: every wave starts holding its share (outstanding = every wave)
+    HX_TRY(reset_sched(pool, ctx.seed ? (uint32_t)grid : 1u, false, (uint32_t)grid));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
     if (int rc0 = check_resident((const void *)k_fib, grid, 64, 0, "hclib_hip_fib")) {
         (void)hipFree(dmem);

@@ -500,6 +500,17 @@ __device__ __forceinline__ void kind_export(const typename Kind::Ctx &ctx, uint3
     if constexpr (kind_has_export<Kind>::value) Kind::export_item(ctx, w, valid, err);
 }
 
+// Optional Kind hooks: static bool seeding(const Ctx&) and
+// template <class WS> static uint32_t seed(const Ctx&, Acc&, WS &stack,
+// uint32_t worker, uint32_t workers, uint32_t spin_ms, uint32_t *err) — the
+// Kind expands its roots itself and leaves each worker's share in its ring
+// (slots 0..n-1, each its own template, child 0); run by every wave of the
+// launch in place of roots() when seeding() holds
+template <class K, class = void>
+struct kind_has_seed : std::false_type {};
+template <class K>
+struct kind_has_seed<K, decltype((void)&K::seeding)> : std::true_type {};
+
 // Optional Kind hook: static void drain(const Ctx&, Acc&, uint32_t *err),
 // called by the whole wave when its ring runs empty, before the wave counts
 // itself idle: work the Kind left in flight across batches (fib's HBM
@@ -1540,6 +1551,20 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             // tree's top levels (the host set outstanding = every wave)
             seeded = true;
             top = seed_levels<Kind, CAP>(ctx, acc, g, st, gid, cfg.nwaves, cfg.spin_limit, n_exec, n_spawn, nbatch, tl);
+            active = true;
+            tl.log(kTlBusy, top);
+            if (top == 0) {
+                active = false;
+                wave_goes_idle<GLOBAL>(g, gv, pool);
+            }
+        }
+    }
+    if constexpr (kind_has_seed<Kind>::value) {
+        // a Kind's own seeding (fib: the call tree's top levels, HBM scopes):
+        // every wave starts with its share; the host set outstanding = every wave
+        if (!seeded && Kind::seeding(ctx)) {
+            seeded = true;
+            top = lane0(Kind::seed(ctx, acc, st, gid, cfg.nwaves, cfg.spin_limit, &g->err));
             active = true;
             tl.log(kTlBusy, top);
             if (top == 0) {

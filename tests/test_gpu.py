@@ -267,14 +267,17 @@ def test_persistent_launch_that_cannot_be_resident_fails_fast(monkeypatch):
                                   {"HCLIB_HIP_FIB_CLIMB": "0", "HCLIB_HIP_FIB_DEFER": "0"},
                                   {"HCLIB_HIP_FIB_CLIMB": "0", "HCLIB_HIP_FIB_DEFER": "1"},
                                   {"HCLIB_HIP_FIB_CLIMB": "1", "HCLIB_HIP_FIB_DEFER": "1"},
-                                  {"HCLIB_HIP_FIB_CLIMB": "3", "HCLIB_HIP_FIB_DEFER": "1"}])
+                                  {"HCLIB_HIP_FIB_CLIMB": "3", "HCLIB_HIP_FIB_DEFER": "1"},
+                                  {"HCLIB_HIP_FIB_SEED": "0"}, {"HCLIB_HIP_FIB_SEED": "1"},
+                                  {"HCLIB_HIP_FIB_SEED": "4", "HCLIB_HIP_WAVES_PER_CU": "2"}])
 def test_fib_finish_scope_modes(mode, monkeypatch):
     """Every join mode gives the same value, tasks and joins: HBM scopes only;
     LDS scopes (hx_finish.h LocalScopes) climbing inline (unbounded, or
     HCLIB_HIP_FIB_CLIMB levels and then as a continuation item) or one level
     per task (continuation items only), with HBM check-outs waited for or
-    resolved a batch later (finish_issue / finish_resolve); fib(25) and
-    fib(30)."""
+    resolved a batch later (finish_issue / finish_resolve); breadth-first
+    seeding of the call tree's top levels (HCLIB_HIP_FIB_SEED items per
+    worker); fib(25) and fib(30)."""
     for k, v in mode.items():
         monkeypatch.setenv(k, v)
     for n, want, calls in [(25, 75025, 242785), (30, 832040, 2692537)]:
