@@ -392,9 +392,11 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
                      // idle-polling waves of the old default fight over crumbs)
                      (uint32_t)env_int("HCLIB_HIP_FIB_CHUNK", 32), FibKind::kWords, &pool));
     SchedConfig cfg;
-    cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_HI", 256);
+    // seeded launches: 320 / 64 (fib(30) 0.49 -> 0.45 ms against 256 / 32,
+    // profiles/r04/fibknobs_f.log, fibknobs_g.log)
+    cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_HI", seed_pw > 0 ? 320 : 256);
     // scripts/sweep_uts.py fib30 (profiles/r01_s5/knob_sweeps.log): 32 -> 1.50 ms, 2 -> 1.70 ms
-    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", 32);
+    cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", seed_pw > 0 ? 64 : 32);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
