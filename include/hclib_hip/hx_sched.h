@@ -903,33 +903,9 @@ __device__ __forceinline__ void carry_lds_slot(uint4 *scr, unsigned long long sp
 template <int TW>
 __device__ __forceinline__ void carry_lds(uint4 *scr, unsigned long long spawn, uint32_t mu, const uint32_t *child,
                                           uint32_t *ctmpl, uint32_t &ck, uint32_t rcp = 0) {
-    static_assert(TW == 2 || TW == 6, "templates are 2 or 6 words");
     const uint32_t lane = (uint32_t)lane_id();
-    const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(spawn >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
-    if ((spawn >> lane) & 1ull) {
-        if constexpr (TW == 6) {
-            scr[2 * rk] = make_uint4(child[0], child[1], child[2], child[3]);
-            *(uint2 *)&scr[2 * rk + 1] = make_uint2(child[4], child[5]);
-        } else {
-            *(uint2 *)&scr[2 * rk] = make_uint2(child[0], child[1]);
-        }
-    }
     const uint32_t r = __umul24(lane, rcp ? rcp : rcp16(mu)) >> 16;  // lane / mu
-    if constexpr (TW == 6) {
-        const uint4 a = scr[2 * r];
-        const uint2 b = *(const uint2 *)&scr[2 * r + 1];
-        ctmpl[0] = a.x;
-        ctmpl[1] = a.y;
-        ctmpl[2] = a.z;
-        ctmpl[3] = a.w;
-        ctmpl[4] = b.x;
-        ctmpl[5] = b.y;
-    } else {
-        const uint2 a = *(const uint2 *)&scr[2 * r];
-        ctmpl[0] = a.x;
-        ctmpl[1] = a.y;
-    }
+    carry_lds_slot<TW>(scr, spawn, child, ctmpl, r);
     ck = lane - __umul24(r, mu);
 }
 
