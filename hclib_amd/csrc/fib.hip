@@ -232,6 +232,13 @@ struct FibKind {
                 cur[0] = (uint32_t)c.n;
                 cur[1] = kScopeRoot;
             }
+            // every scope the seeding can open (< target: a binary tree of
+            // fewer than `target` leaves), taken with one atomic
+            uint32_t base = 0, used = 0;
+            if (lane == 0) base = add_agent(c.fin.next, target);
+            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+            const bool ids_ok = base + target <= c.fin.cap;
+            if (!ids_ok && lane == 0) dev_error(err, kErrArena);
             uint32_t cnt = 1;
             while (cnt > 0 && 2 * cnt <= target) {
                 uint32_t ncnt = 0;
@@ -239,11 +246,18 @@ struct FibKind {
                     const uint32_t i = b + lane;
                     const bool has = i < cnt;
                     const uint32_t m = has ? cur[2 * i] : 0u, p = has ? cur[2 * i + 1] : kScopeRoot;
-                    const bool open = has && m >= 2;
-                    const uint32_t S = finish_open(c.fin, open, p, 2, 0, err, c.blocks ? s_fib_blk : nullptr);
+                    const bool open = has && m >= 2 && ids_ok;
                     const unsigned long long om = __ballot(open);
                     const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32),
                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u));
+                    const uint32_t S = base + used + rk;
+                    used += (uint32_t)__popcll(om);
+                    if (open) {  // (as finish_open: count 2, no continuation)
+                        FinishScope *f = &c.fin.scopes[S];
+                        st_agent(&f->word, 2ull << 56);
+                        st_agent(&f->parent, p);
+                        st_agent(&f->cont, 0u);
+                    }
                     if (open) {
                         const uint32_t o = ncnt + 2 * rk;
                         nxt[2 * o] = m - 1;
