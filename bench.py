@@ -340,7 +340,9 @@ def cpu_baseline(allot, min_seconds=10.0):
     # timed it beside this port on T3L
     out["reference_cross_check"] = {
         "source": "round-3 review (VERDICT.md): reference built out of tree with its CMake, test/uts/UTS.cpp "
-                  "with the survey's driver shims, T3L, same container",
+                  "with the survey's driver shims, T3L; both runs on the review's 8-core Xeon build container, "
+                  "not on this GPU box's host",
+        "host": "8-core Xeon build container (no GPU); the port-vs-reference ratio is specific to that host",
         "reference_nodes_per_s_8_workers": [22.6e6, 24.4e6], "port_nodes_per_s_8_workers": [35.5e6, 40.2e6],
         "reference_nodes_per_s_1_worker": 3.88e6, "port_nodes_per_s_1_worker": 3.9e6,
         "port_over_reference_8_workers": 1.6,
@@ -425,39 +427,27 @@ def sharded_sw(H, rank, world, be, steps=2):
     # exercise). The RCCL path cannot run on a 1-GPU box (two RCCL ranks need
     # two devices): if it raises, the leg falls back to gloo and says why.
     xbe = os.environ.get("HCLIB_BENCH_SW_EXCHANGE", be)
-    import torch.distributed as tdist
 
-    def measure(xb):
-        group = tdist.new_group(backend="gloo") if (xb == "gloo" and be != "gloo") else None
-        best = None
-        for _ in range(steps):
-            job = dist.ShardedSw(s1, s2, 256, 256, rank, world, xb, block_rows=k, group=group)
-            dist.barrier(world, be)
-            t0 = time.perf_counter()
-            score, tiles = job.run()
-            dist.barrier(world, be)
-            ms = dist.max_over_ranks((time.perf_counter() - t0) * 1e3, world, be)
-            if score != 128772 or tiles != 65536:
-                raise SystemExit(f"sharded SW mismatch: score {score}, tiles {tiles}")
-            best = ms if best is None else min(best, ms)
-        return best
+    def make_job(xb, group, abort):
+        return dist.ShardedSw(s1, s2, 256, 256, rank, world, xb, block_rows=k, group=group, abort=abort)
 
-    fallback = None
-    try:
-        best = measure(xbe)
-    except Exception as e:  # noqa: BLE001
-        if xbe != "nccl":
-            raise
-        fallback = f"RCCL exchange failed ({type(e).__name__}: {str(e)[:200]}); measured over gloo"
-        xbe = "gloo"
-        best = measure(xbe)
+    # the ranks agree on any fallback through the rendezvous store and a gloo
+    # control group (dist.sw_exchange): never one-sided, never on an RCCL
+    # group an error may have aborted
+    res = dist.sw_exchange(make_job, rank, world, xbe, (128772, 65536), steps=steps)
     out = {"workload": f"test/smithwaterman 64K x 64K, 256x256 tiles, {world} column bands, "
                        f"{k} tile rows per exchanged block",
-           "exchange": "RCCL send/recv (xGMI)" if xbe == "nccl" else "gloo send/recv staged through host memory",
-           "cells_per_s": 65536.0 * 65536.0 / (best * 1e-3), "ms": best, "score": 128772,
-           "bit_exact": True, "scaling": "strong", "bound": "span"}
-    if fallback:
-        out["fallback"] = fallback
+           "exchange": "RCCL send/recv (xGMI)" if res["exchange"] == "nccl" else
+                       "gloo send/recv staged through host memory",
+           "scaling": "strong", "bound": "span"}
+    if "failed" in res:
+        out["failed"] = res["failed"]
+        return out
+    best = res["ms"]
+    out.update({"cells_per_s": 65536.0 * 65536.0 / (best * 1e-3), "ms": best, "score": 128772,
+                "bit_exact": True})
+    if "fallback" in res:
+        out["fallback"] = res["fallback"]
     return out
 
 
@@ -544,10 +534,14 @@ def main():
     skewed = None
     if world > 1 and not args.no_extras and os.environ.get("HCLIB_BENCH_SHARE_WORK", "1") != "0":
         skewed = guarded("uts_work_sharing", lambda: skewed_sharing(H, rank, world, be))
-    stalled = bool(legs and legs.stalled)
+    # a stall anywhere (this rank's guard, or another rank's flag in the
+    # store) ends every rank the same way: no orderly shutdown (a leg's thread
+    # may still sit in a collective) and a non-zero exit status, so torchrun
+    # and the driver see the run as failed; rank 0 prints its line first
+    stalled = bool(legs and (legs.stalled or legs.peer_stalled()))
     if rank != 0:
-        if stalled:  # a leg's thread may still sit in a collective: no orderly shutdown
-            os._exit(0)
+        if stalled:
+            os._exit(3)
         dist.shutdown(world)
         return
 
@@ -673,7 +667,7 @@ def main():
         out["cpu_configs"] = cpu_configs(allot["threads"], s1, s2, out["configs"])
     print(json.dumps(out), flush=True)
     if stalled:
-        os._exit(0)
+        os._exit(3)
     dist.shutdown(world)
 
 

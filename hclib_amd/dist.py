@@ -61,7 +61,7 @@ class LegGuard:
     is blocked), after which every rank skips the remaining legs. A leg that
     raises is reported with its exception. The caller prints its line and,
     when `stalled`, leaves with os._exit (a blocked collective thread would
-    hold a normal shutdown)."""
+    hold a normal shutdown) and a non-zero status (bench.py: 3)."""
 
     KEY = "hclib_leg_stalled"
 
@@ -77,7 +77,7 @@ class LegGuard:
             except Exception:  # noqa: BLE001 (no store: each rank only knows its own stalls)
                 self.store = None
 
-    def _peer_stalled(self) -> bool:
+    def peer_stalled(self) -> bool:
         if self.store is None:
             return False
         try:
@@ -87,7 +87,7 @@ class LegGuard:
 
     def run(self, name: str, fn):
         """fn() -> dict; returns its result or {"failed": reason}."""
-        if self.stalled or self._peer_stalled():
+        if self.stalled or self.peer_stalled():
             self.stalled = True
             return {"failed": "skipped: an earlier leg stalled on some rank"}
         box = {}
@@ -254,20 +254,29 @@ class _HipBand:
         return self.band.end(self.stream)
 
 
+class ExchangeAborted(RuntimeError):
+    """Another rank gave up on the column exchange (sw_exchange)."""
+
+
 class ShardedSw:
     """One rank's share of a sharded SW run. __init__ uploads the band
     (outside any timed region); run() executes the pipeline once and
     returns (score, tiles over all ranks). `band_factory(s1, s2, tw, th, j0,
     j1)` defaults to the HIP band; the CPU tests pass a host DP band.
     `group` (default: the world group) carries the exchange; `backend` is
-    that group's backend ("gloo" stages the columns through host memory)."""
+    that group's backend ("gloo" stages the columns through host memory).
+    `abort` (optional, () -> reason or None) is polled while this rank waits
+    on the exchange: a peer that failed sets it (sw_exchange), and the wait
+    ends with ExchangeAborted instead of blocking until the group's timeout.
+    `inject` (tests only) is called before each receive."""
 
     def __init__(self, s1: bytes, s2: bytes, tw: int, th: int, rank: int, world: int,
                  backend: str = "nccl", block_rows: int = 16, band_factory=None, device=None,
-                 group=None):
+                 group=None, abort=None, inject=None):
         import torch
 
         self.rank, self.world, self.backend, self.group = rank, world, backend, group
+        self.abort, self.inject = abort, inject
         self.th = th
         ntw, nth = len(s1) // tw, len(s2) // th
         self.j0, self.j1 = sw_bands(ntw, world)[rank]
@@ -280,24 +289,72 @@ class ShardedSw:
         self.right = torch.empty(n, dtype=torch.int32, device=device) if rank < world - 1 else None
         self.band = (band_factory or _HipBand)(s1, s2, tw, th, self.j0, self.j1)
 
+    def _wait(self, work):
+        """Host wait on a gloo transfer, bounded by the peers: polls the
+        transfer and `abort` instead of blocking in work.wait()."""
+        if self.abort is None:
+            work.wait()
+            return
+        # gloo's send/recv works complete only inside wait(): it runs on a
+        # helper thread while this one polls `abort` (an aborted wait is left
+        # behind on its daemon thread)
+        box = {}
+
+        def waiter():
+            try:
+                work.wait()
+            except BaseException as e:  # noqa: BLE001 (re-raised on the caller's thread)
+                box["e"] = e
+        th = threading.Thread(target=waiter, daemon=True)
+        th.start()
+        th.join(0.002)
+        while th.is_alive():
+            why = self.abort()
+            if why:
+                raise ExchangeAborted(why)
+            th.join(0.0005)
+        if "e" in box:
+            raise box["e"]
+
     def _recv(self, t):
         import torch
         import torch.distributed as dist
 
-        if self.backend == "nccl" or t.device.type == "cpu":
-            dist.recv(t, src=self.rank - 1, group=self.group)
+        if self.inject is not None:
+            self.inject()
+        if self.backend == "nccl":
+            dist.recv(t, src=self.rank - 1, group=self.group)  # stream-ordered: the host does not wait
+        elif t.device.type == "cpu":
+            self._wait(dist.irecv(t, src=self.rank - 1, group=self.group))
         else:  # gloo carries host tensors only
             h = torch.empty_like(t, device="cpu")
-            dist.recv(h, src=self.rank - 1, group=self.group)
+            self._wait(dist.irecv(h, src=self.rank - 1, group=self.group))
             t.copy_(h)
 
     def _send(self, t):
         import torch.distributed as dist
 
-        if self.backend == "nccl" or t.device.type == "cpu":
+        if self.backend == "nccl":
             dist.send(t, dst=self.rank + 1, group=self.group)
         else:
-            dist.send(t.cpu(), dst=self.rank + 1, group=self.group)
+            self._wait(dist.isend(t if t.device.type == "cpu" else t.cpu(), dst=self.rank + 1, group=self.group))
+
+    def _drain(self):
+        """RCCL: the host waits for the band's stream (kernels, sends, receives)
+        by polling an event and `abort`, so a peer's failure ends the wait."""
+        import time
+
+        import torch
+
+        if self.abort is None or self.backend != "nccl":
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        while not ev.query():
+            why = self.abort()
+            if why:
+                raise ExchangeAborted(why)
+            time.sleep(0.0005)
 
     def run(self):
         import contextlib
@@ -317,6 +374,7 @@ class ShardedSw:
                 self.band.rows(i0, i1, self.left, self.right)
                 if self.right is not None:
                     self._send(self.right[i0 * th:i1 * th])
+            self._drain()
             corner, tiles = self.band.end()
         if self.world == 1:
             return corner, tiles
@@ -324,10 +382,109 @@ class ShardedSw:
 
         dev = _device(self.backend)
         sc = torch.tensor([corner if self.rank == self.world - 1 else 0], dtype=torch.int64, device=dev)
-        dist.broadcast(sc, src=self.world - 1, group=self.group)
         tt = torch.tensor([tiles], dtype=torch.int64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.SUM, group=self.group)
+        if self.backend == "nccl":
+            dist.broadcast(sc, src=self.world - 1, group=self.group)
+            dist.all_reduce(tt, op=dist.ReduceOp.SUM, group=self.group)
+            self._drain()  # a peer that failed ends this wait too
+        else:
+            self._wait(dist.broadcast(sc, src=self.world - 1, group=self.group, async_op=True))
+            self._wait(dist.all_reduce(tt, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         return int(sc[0]), int(tt[0])
+
+
+def sw_exchange(make_job, rank: int, world: int, backend: str, expected, steps: int = 2, store=None,
+                key: str = "hclib_sw_x"):
+    """Measure a sharded SW run (best of `steps`, ms over the slowest rank)
+    with its column exchange on `backend`, falling back to gloo TOGETHER if
+    any rank's attempt fails.
+
+    make_job(backend, group, abort) -> ShardedSw; `expected` = its run()'s
+    (score, tiles). Each attempt's exchange runs on a group of its own (a
+    failed RCCL one is aborted before the gloo attempt). Everything that decides or
+    times lives on a gloo control group created here (never on an RCCL group
+    an error may have aborted): the barriers around each run, the max over
+    ranks, and the agreement after the attempt. A rank whose attempt raises
+    sets `key` in the rendezvous store; the others' exchange waits poll that
+    key (ShardedSw `abort`) and stop within milliseconds. Every rank then
+    meets on the control group, and if any failed all re-measure over a
+    fresh gloo exchange group. Returns {"ms", "exchange", "fallback"?} or
+    {"failed": reason} when the gloo attempt fails as well."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    if store is None:
+        store = dist.distributed_c10d._get_default_store()
+    ctrl = dist.new_group(backend="gloo")  # collective: every rank, same order
+
+    def abort_of(k):
+        def check():
+            try:
+                if store.check([k]):
+                    return store.get(k).decode(errors="replace")
+            except Exception:  # noqa: BLE001 (a store we cannot read never aborts)
+                return None
+            return None
+        return check
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        dist.barrier(group=ctrl)
+
+    def maxr(x):
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctrl)
+        return float(t[0])
+
+    def attempt(xb, k):
+        group = dist.new_group(backend=xb)  # collective; a fresh group per attempt
+        err = None
+        best = None
+        try:
+            for _ in range(steps):
+                job = make_job(xb, group, abort_of(k))
+                sync()
+                t0 = time.perf_counter()
+                score, tiles = job.run()
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+                ms = (time.perf_counter() - t0) * 1e3
+                if (score, tiles) != tuple(expected):
+                    raise RuntimeError(f"mismatch: score {score}, tiles {tiles}, want {tuple(expected)}")
+                best = ms if best is None else min(best, ms)
+        except Exception as e:  # noqa: BLE001 (agreed on below, every rank reaches the control group)
+            err = f"rank {rank}: {type(e).__name__}: {str(e)[:200]}"
+            if not isinstance(e, ExchangeAborted):
+                try:
+                    store.set(k, err)
+                except Exception:  # noqa: BLE001
+                    pass
+        failed = maxr(1.0 if (err or abort_of(k)()) else 0.0) != 0.0
+        if failed:
+            if xb == "nccl":
+                # kernels of the failed exchange may still wait on the band's
+                # stream: abort the communicator so they end (best effort)
+                try:
+                    dist.distributed_c10d._abort_process_group(group)
+                except Exception:  # noqa: BLE001
+                    pass
+            return None, abort_of(k)() or err or "failed on another rank"
+        return maxr(best), None
+
+    ms, why = attempt(backend, key)
+    out = {"exchange": backend}
+    if why is None:
+        out["ms"] = ms
+        return out
+    out["fallback"] = f"{backend} exchange failed ({why}); measured over gloo on every rank"
+    ms2, why2 = attempt("gloo", key + "_fallback")
+    if why2 is not None:
+        return {"failed": f"{out['fallback']}; gloo also failed: {why2}", "exchange": "gloo"}
+    out.update({"ms": ms2, "exchange": "gloo"})
+    return out
 
 
 class GlobalPool:

@@ -253,3 +253,71 @@ def test_stalled_leg_is_reported_and_the_line_still_prints():
         assert b["failed"].startswith("skipped"), (r, b)
         assert stalled
         assert el < 30, el  # the guard's bound (4 s per leg), not the collective's 60 s
+
+
+# ------------------------------------------- SW exchange fallback is collective
+# bench.py's sharded SW leg (dist.sw_exchange): rank 1's exchange raises on
+# its first receive of the primary attempt while rank 0 is blocked sending to
+# it. Rank 1 flags the failure in the rendezvous store, rank 0's send wait
+# sees the flag and stops, both agree on a gloo control group and re-measure
+# together over a fresh gloo exchange group; the result is exact and the
+# whole leg ends within seconds (not the group's 60 s timeout).
+def _sw_fallback_worker(rank, world, port, s1, s2, tw, th, q, fail_gloo_too):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HCLIB_DIST_TIMEOUT_S": "60"})
+    import time
+
+    import torch
+
+    from hclib_amd import dist
+
+    r, w, _ = dist.init_from_env("gloo")
+    attempts = []
+
+    def make_job(xb, group, abort):
+        attempts.append(xb)
+        first = len(attempts) == 1
+
+        def inject():
+            if r == 1 and (first or fail_gloo_too):
+                raise RuntimeError("injected exchange failure")
+        return dist.ShardedSw(s1, s2, tw, th, r, w, xb, 1, band_factory=_HostBand, device=torch.device("cpu"),
+                              group=group, abort=abort, inject=inject)
+
+    want = (__import__("oracle.loader", fromlist=["sw_score"]).sw_score(s1, s2, tw, th), (len(s1) // tw) * (len(s2) // th))
+    t0 = time.monotonic()
+    res = dist.sw_exchange(make_job, r, w, "gloo", want, steps=1)
+    el = time.monotonic() - t0
+    q.put((r, res, el, attempts))
+    q.close()
+    q.join_thread()
+    os._exit(0)  # abandoned transfers of the failed attempt: no orderly shutdown
+
+
+@pytest.mark.parametrize("fail_gloo_too", [False, True])
+def test_sw_exchange_failure_falls_back_on_every_rank(fail_gloo_too):
+    import random
+
+    rng = random.Random(7)
+    tw, th = 8, 6
+    s1 = bytes(rng.randint(1, 4) for _ in range(4 * tw))
+    s2 = bytes(rng.randint(1, 4) for _ in range(5 * th))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sw_fallback_worker, args=(r, 2, port, s1, s2, tw, th, q, fail_gloo_too))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r, out, el, attempts in res:
+        assert el < 10.0, (r, el)
+        assert attempts == ["gloo", "gloo"], (r, attempts)  # both ranks re-ran, together
+        if fail_gloo_too:
+            assert "failed" in out and "injected" in out["failed"], (r, out)
+        else:
+            assert "injected exchange failure" in out["fallback"], (r, out)
+            assert out["exchange"] == "gloo" and out["ms"] > 0
