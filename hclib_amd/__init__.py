@@ -63,6 +63,14 @@ class UtsResult(C.Structure):
     ]
 
 
+class UtsLaunch(C.Structure):
+    _fields_ = [(k, C.c_int) for k in ("mode", "feat", "workers_per_group", "grid", "ring", "seeded",
+                                       "seed_target", "spill_lo", "waves_per_cu")]
+
+
+UTS_MODES = {0: "rules_global", 1: "rules_lds", 2: "bin", 3: "geo_fixed"}
+
+
 class FibResult(C.Structure):
     _fields_ = [("tasks", C.c_uint64), ("joins", C.c_uint64), ("chunks_pushed", C.c_uint64),
                 ("chunks_stolen", C.c_uint64), ("kernel_ms", C.c_double),
@@ -122,6 +130,7 @@ def lib():
                                                  C.POINTER(C.c_double)]
         L.hclib_hip_sha1_calibrate.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double),
                                                C.POINTER(C.c_double)]
+        L.hclib_hip_uts_last_launch.argtypes = [C.POINTER(UtsLaunch)]
         L.hclib_hip_uts_bucket_check.argtypes = [C.POINTER(UtsParams), C.c_uint64, C.POINTER(C.c_uint64)]
         L.hclib_hip_global_bytes.restype = C.c_size_t
         L.hclib_hip_global_bytes.argtypes = [C.c_uint32]
@@ -211,6 +220,15 @@ def uts(params, shard: int = 0, nshards: int = 1, split_depth: int = 0, max_leve
     out = {k: getattr(r, k) for k, _ in UtsResult._fields_}
     if hist is not None:
         out["levels"] = list(hist)
+    return out
+
+
+def uts_last_launch() -> dict:
+    """The launch shape of this thread's last uts() (hclib_hip_uts_last_launch)."""
+    r = UtsLaunch()
+    _check(lib().hclib_hip_uts_last_launch(C.byref(r)), "hclib_hip_uts_last_launch")
+    out = {k: getattr(r, k) for k, _ in UtsLaunch._fields_}
+    out["mode"] = UTS_MODES.get(out["mode"], out["mode"])
     return out
 
 

@@ -21,9 +21,9 @@ namespace hx {
 
 struct FibCtx {
     int n;
-    int local;  // scopes in the wave's LDS while they stay inside it (hx_finish.h LocalScopes)
-    int defer;  // HBM check-out steps issued in one batch, resolved in the next (finish_issue)
-    int climb;  // LDS mode: scopes a leaf completes inline (then, or with 0 at once, kFibCont items)
+    int local;  // scopes in the wave's LDS while they stay inside it (hx_finish.h LocalScopes);
+                // their HBM check-out steps are issued in one batch and resolved in the next
+                // (finish_issue / finish_resolve)
     int blocks; // HBM scope ids taken kScopeBlock at a time per wave
     uint32_t *seed;     // breadth-first seeding (HCLIB_HIP_FIB_SEED): [0] ready flag, [1] items, [64..] items; or null
     int seed_per_wave;  // ... items per worker it aims at
@@ -48,14 +48,14 @@ struct FibKind {
     static constexpr int kTmplWords = 2;
     static constexpr int kWords = 4;
     static constexpr bool kPure = false;           // scopes are opened / checked out in HBM
-    static constexpr bool kBoundedChildren = true;  // 0, 1 (a continuation item) or 2
+    static constexpr bool kBoundedChildren = true;  // 0 or 2
 #ifdef HX_FIB_PIECES
     static constexpr int kPieces = HX_FIB_PIECES;  // (small-ring builds: a lane's batch output bound)
 #endif
     using Ctx = FibCtx;
     struct Acc {
         unsigned long long tasks = 0, joins = 0;
-        FinishInFlight q;  // this lane's HBM check-out step in flight (FibCtx::defer)
+        FinishInFlight q;  // this lane's HBM check-out step in flight (LDS mode)
         // HX_STAMPS builds: cycles in process's phases (resolve, open, check-out), first active lane only
         unsigned long long cyc[3] = {0, 0, 0};
         // the wave's totals go into its exit record (hx_sched.h Kind concept)
@@ -75,39 +75,6 @@ struct FibKind {
         return 1;
     }
 
-    // LDS mode: a scope's climb runs one level per task. The last task out of
-    // scope s pushes the continuation item {kFibCont, s} (its sum is in s's
-    // word), which frees s and checks out of s's parent in a later batch: a
-    // batch waits for one check-out per lane, not for its longest chain
-    static constexpr uint32_t kFibCont = 0xFFFFFFFFu;
-
-    // one check-out step of v from scope s; true: s's last task is out (LDS s)
-    __device__ static bool check_out_one(const Ctx &c, Acc &acc, uint32_t s, unsigned long long v) {
-        v &= kScopeSumMask;
-        if (s == kScopeRoot) {
-            st_agent(c.fin.root_value, v);
-            return false;
-        }
-        if (scope_is_lds(s)) {
-            const uint32_t slot = s & (kScopeLds - 1);
-            if (slot >= (uint32_t)kFibLocalScopes) return false;  // (never)
-            // the atomic first, the record read behind it (one round trip)
-            unsigned long long old = __hip_atomic_fetch_add(&s_fib_scopes.word[slot], v - kScopeOne, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
-            const hx_u32x4 meta = s_fib_scopes.meta[slot];
-            if (!meta.z) {
-                if ((old & kScopeSumMask) + v > kScopeSumMask)  // see finish_check_out
-                    old = __hip_atomic_fetch_add(&s_fib_scopes.word[slot], (unsigned long long)0 - kScopeOne,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                return (old >> 56) == 1;
-            }
-            s = meta.z - 1;  // promoted: the HBM copy counts (the LDS add is harmless)
-        }
-        if (c.defer && acc.q.s == kScopeRoot) finish_issue(c.fin, acc.q, s, v);
-        else acc.joins += finish_check_out(c.fin, s, v, PassSum());
-        return false;
-    }
-
     __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
                                   uint32_t *child, uint32_t *err, bool) {
 #if defined(HX_STAMPS) && HX_STAMPS
@@ -124,12 +91,11 @@ struct FibKind {
         unsigned long long tst = 0;
         stamp(-1, tst);
         // the HBM check-out this lane issued a batch ago: its result is in
-        if (c.defer) acc.joins += finish_resolve(c.fin, acc.q, PassSum());
+        if (c.local) acc.joins += finish_resolve(c.fin, acc.q, PassSum());
         stamp(0, tst);
-        const bool cont_item = c.local && t[0] == kFibCont;
-        const int n = cont_item ? 0 : (int)t[0] - 1 - (int)k;
-        const bool spawn = !cont_item && n >= 2;
-        if (!cont_item) acc.tasks += 1;
+        const int n = (int)t[0] - 1 - (int)k;
+        const bool spawn = n >= 2;
+        acc.tasks += 1;
         // FINISH { async fib(n-1); async fib(n-2); }  (one bump allocation
         // per wave for every lane that opens a scope)
         const uint32_t j = c.local ? finish_open_local(c.fin, s_fib_scopes, spawn, t[1], 2, 0, err,
@@ -142,71 +108,24 @@ struct FibKind {
             child[1] = j;
             return 2;
         }
-        if (!c.local || (c.climb && !cont_item)) {  // a leaf returns n: check out, continuations inline
-            const bool busy = acc.q.s != kScopeRoot;
-            stamp(-1, tst);
+        // a leaf returns n: it checks out, and the last task out of each scope
+        // runs its continuation inline, up the chain (an unbounded climb:
+        // round 4 measured bounded climbs and one level per continuation item
+        // no faster)
+        stamp(-1, tst);
 #if defined(HX_STAMPS) && HX_STAMPS
-            uint32_t steps = 0;
-            uint32_t *stp = lead ? &steps : nullptr;
+        uint32_t steps = 0;
+        uint32_t *stp = lead ? &steps : nullptr;
 #else
-            uint32_t *stp = nullptr;
+        uint32_t *stp = nullptr;
 #endif
-            uint32_t pend = kScopeRoot;  // a completed scope past c.climb levels: continued as an item
-            acc.joins += c.local ? finish_check_out_local(c.fin, s_fib_scopes, t[1], (unsigned long long)n, PassSum(),
-                                                          c.defer ? &acc.q : nullptr, stp, (uint32_t)c.climb, &pend)
-                                 : finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
-            stamp(1, tst);
+        acc.joins += c.local ? finish_check_out_local(c.fin, s_fib_scopes, t[1], (unsigned long long)n, PassSum(),
+                                                      &acc.q, stp)
+                             : finish_check_out(c.fin, t[1], (unsigned long long)n, PassSum());
+        stamp(1, tst);
 #if defined(HX_STAMPS) && HX_STAMPS
-            acc.cyc[2] += steps;  // (c[3]: lock-step iterations, first active lane)
+        acc.cyc[2] += steps;  // (c[3]: lock-step iterations, first active lane)
 #endif
-            (void)busy;
-            if (pend != kScopeRoot) {
-                child[0] = kFibCont;
-                child[1] = pend;
-                return 1;
-            }
-            return 0;
-        }
-        // a leaf checks n out of its scope; a continuation item frees its
-        // scope and checks the scope's sum out of the parent
-        uint32_t s = t[1], slot = 0;
-        unsigned long long v = (unsigned long long)n;
-        bool freeing = false;
-        if (cont_item) {
-            uint32_t x = t[1];
-            if (scope_is_lds(x)) {
-                slot = x & (kScopeLds - 1);
-                const hx_u32x4 meta = s_fib_scopes.meta[slot < (uint32_t)kFibLocalScopes ? slot : 0];
-                if (meta.z) x = meta.z - 1;  // (promoted: the HBM copy holds the sum)
-                else {
-                    v = s_fib_scopes.word[slot] & kScopeSumMask;  // PassSum: cont(_, sum) = sum
-                    s = meta.x;
-                    freeing = true;
-                }
-            }
-            if (!freeing) {  // an HBM scope (an exported continuation item)
-                const FinishScope *f = &c.fin.scopes[x];
-                v = ld_agent(&f->word) & kScopeSumMask;
-                s = ld_agent(&f->parent);
-            }
-            acc.joins += 1;
-        }
-        // the freed slots onto the free list by ballot rank
-        const unsigned long long fm = __ballot(freeing);
-        if (fm) {
-            const uint32_t nf = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_fib_scopes.nfree);
-            if (freeing)
-                s_fib_scopes.freelist[nf + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u))] = slot;
-            s_fib_scopes.nfree = nf + (uint32_t)__popcll(fm);
-        }
-        const bool last = check_out_one(c, acc, s, v);
-        stamp(2, tst);
-        if (last) {
-            child[0] = kFibCont;
-            child[1] = s;
-            return 1;
-        }
         return 0;
     }
 
@@ -308,7 +227,7 @@ struct FibKind {
 
     // the ring ran empty: the check-outs still in flight, to their ends
     __device__ static void drain(const Ctx &c, Acc &acc, uint32_t *) {
-        if (c.defer) acc.joins += finish_drain(c.fin, acc.q, PassSum());
+        if (c.local) acc.joins += finish_drain(c.fin, acc.q, PassSum());
     }
 
     // an item leaving the wave names an HBM scope (its LDS scope promoted)
@@ -361,8 +280,12 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     const int grid = env_int("HCLIB_HIP_GRID", 0) > 0 ? env_int("HCLIB_HIP_GRID", 0)
                                                     : m.num_cus * env_int("HCLIB_HIP_WAVES_PER_CU", 3);
     const int blocks = env_int("HCLIB_HIP_FIB_BLOCKS", 1);
-    // the arena: every scope once, plus each wave's last partly used id block
-    const unsigned long long ids = scopes + 1 + (blocks ? (unsigned long long)grid * kScopeBlock : 0ull);
+    // the arena: every scope once, plus each wave's last partly used id block,
+    // plus the seeding's reservation (worker 0 takes up to kFibSeedCap ids in
+    // one atomic and opens only as many as its levels need)
+    const int seed_pw = env_int("HCLIB_HIP_FIB_SEED", 2);
+    const unsigned long long ids = scopes + 1 + (blocks ? (unsigned long long)grid * kScopeBlock : 0ull) +
+                                   (seed_pw > 0 ? (unsigned long long)kFibSeedCap : 0ull);
     if (ids > 0xfffffff0ull) {
         set_error("hclib_hip_fib: n too large for the join arena");
         return HCLIB_HIP_EINVAL;
@@ -371,7 +294,6 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     // seeding buffer behind the arena's counters: [0] flag, [1] count, [64..] items
     // (2 items per worker, at most kFibSeedCap: fib(30) 0.70-0.74 -> 0.47-0.49 ms,
     // profiles/r04/fibseed_sweep.log, fibseed2_sweep.log; 0: from one root)
-    const int seed_pw = env_int("HCLIB_HIP_FIB_SEED", 2);
     const size_t sb = seed_pw > 0 ? (64 + 2 * (size_t)kFibSeedCap) * 4 : 0;
     void *dmem = nullptr;
     HX_HIP(hipMalloc(&dmem, jb + 512 + sb));
@@ -380,12 +302,6 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     // LDS scopes (hx_finish.h LocalScopes, batched promotion): fib(30)
     // 0.807 -> 0.688 ms (profiles/r04/fiblds_sweep.log)
     ctx.local = env_int("HCLIB_HIP_FIB_LOCAL", 1);
-    ctx.defer = ctx.local && env_int("HCLIB_HIP_FIB_DEFER", 1);
-    // LDS scopes a leaf's check-out completes inline before it hands the
-    // climb on as a continuation item (0: one level per task, every climb an
-    // item). Inline vs items: 0.69-0.74 ms both, same box
-    // (profiles/r04/fibclimb_sweep.log); the inline walk runs fewer batches
-    ctx.climb = env_int("HCLIB_HIP_FIB_CLIMB", 1 << 30);
     ctx.fin.scopes = (FinishScope *)dmem;
     ctx.fin.next = (uint32_t *)((char *)dmem + ((jb + 255) & ~(size_t)255));
     ctx.fin.cap = (uint32_t)ids;
@@ -415,11 +331,6 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_FIB_HUNGER", 8);
-    // ramp-up / tail (more than 1/8 of the waves hungry): spill threshold,
-    // chunk size and hunger-read interval then (0: the steady-state values)
-    cfg.spill_lo_hungry = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO_HUNGRY", 0);
-    cfg.ramp_chunk = (uint32_t)env_int("HCLIB_HIP_FIB_RAMP_CHUNK", 0);
-    cfg.hunger_fast = (uint32_t)env_int("HCLIB_HIP_FIB_HUNGER_FAST", 0);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 1);
     // seeded: every wave starts holding its share (outstanding = every wave)
     HX_TRY(reset_sched(pool, ctx.seed ? (uint32_t)grid : 1u, false, (uint32_t)grid));

@@ -1387,7 +1387,7 @@ __device__ __forceinline__ bool sw_pk_wait(const SwCtx &c, const int *flag, int 
 // workgroup keeps when its own put releases it) while the sweep still runs.
 // `mid` runs once the columns the first chunk reads (x < 64) and the score
 // rows are staged (the first chunk's scores can start before the rest).
-template <int KX, class Mid, bool P2 = false>
+template <int KX, class Mid>
 __device__ bool sw_pk_stage(const SwCtx &c, int R0, int C0, int ncols, int *sel, int *tbl, Mid &&mid) {
     const int lane = lane_id();
     const int selw = sw_pk_selw(ncols), xmax = ncols - 1;
@@ -1397,11 +1397,9 @@ __device__ bool sw_pk_stage(const SwCtx &c, int R0, int C0, int ncols, int *sel,
         const int x = lane + 64 * k;
         code[k] = (int)c.s1[C0 + (x < ncols ? x : xmax)];
     }
-    // this lane's rows: lo q0, lo q1, hi q0, hi q1 (as the sweep wave's);
-    // P2 (two sweep waves, sw_pk2_tile): A lo, B lo, A hi, B hi
+    // this lane's rows: lo q0, lo q1, hi q0, hi q1 (as the sweep wave's)
     const int r0 = R0 + 1 + 2 * lane;
-    const int s2a = P2 ? c.s2[R0 + lane] : c.s2[r0 - 1], s2b = P2 ? c.s2[R0 + 128 + lane] : c.s2[r0],
-              s2c = P2 ? c.s2[R0 + 64 + lane] : c.s2[r0 + 127], s2d = P2 ? c.s2[R0 + 192 + lane] : c.s2[r0 + 128];
+    const int s2a = c.s2[r0 - 1], s2b = c.s2[r0], s2c = c.s2[r0 + 127], s2d = c.s2[r0 + 128];
 #pragma unroll
     for (int k = 0; k < KX; ++k)
         if (lane + 64 * k >= ncols) code[k] = (int)kSwPkNull;
@@ -1650,250 +1648,6 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
     return true;
 }
 
-// ---- two sweep waves. A lone wave issues one VALU
-// operation per ~5 cycles (profiles/r04/ub_valu2.log), so the one-wave body's
-// step (two dependent packed pairs per lane, 54 cycles) is issue-bound. Here
-// wave A sweeps the tile's rows 1..128 and wave B rows 129..256, each lane
-// one packed pair {row 128h + L + 1, row 128h + L + 65} (the high row 64
-// steps behind, as in sw_pk_tile): a step is one rotate, one v_perm, one
-// v_pk_add and one v_pk_maximum3 per wave, on two SIMDs. B's top row (row
-// 128 of the tile) is A's lane 63 high half: A publishes it into LDS every 16
-// steps (lanes 56..63 of the bottom-row accumulator), B trails A by ~150
-// steps and waits on misc[10] (columns published) every half chunk. The
-// score wave feeds both through rings of their own: A's 2 chunks, B's 4
-// (B consumes each chunk ~2.5 chunks after A).
-constexpr int kSwPk2SlotsA = 2, kSwPk2SlotsB = 4;
-constexpr int kSwPk2RingU4 = (kSwPk2SlotsA + kSwPk2SlotsB) * 16 * 64;  // uint4: 64 steps x 64 lanes / 4 per chunk
-// LDS: ring A | ring B | top A | top B | sel x 4 | right columns [2][256] | dummy[64] | misc[16] | score rows [4][64] | next top row [512]
-__host__ __device__ constexpr int sw_pk2_lds_words(int tw) {
-    return kSwPk2RingU4 * 4 + 2 * sw_pk_topw(tw) + 4 * sw_pk_selw(tw) + 2 * kSwPkTh + 64 + kSwPkMisc + 256 + kSwPkMaxTw;
-}
-inline size_t sw_pk2_lds_bytes(int tw) { return (size_t)sw_pk2_lds_words(tw) * 4; }
-
-// The score wave of the two-sweep body: every chunk's words for A and B.
-// misc[6] / misc[9] = chunks A / B have read, misc[5] = chunks written.
-__device__ bool sw_pk2_scores(const SwCtx &c, int ncols, uint4 *ringA, uint4 *ringB, const int *sel, const int *tbl,
-                              int *misc, int k0 = 0, int k1 = 1 << 30) {
-    const int lane = lane_id();
-    const int selw = sw_pk_selw(ncols);
-    const uint32_t mloA = (uint32_t)tbl[lane], mloB = (uint32_t)tbl[64 + lane];
-    const uint32_t mhiA = (uint32_t)tbl[128 + lane], mhiB = (uint32_t)tbl[192 + lane];
-    const int *selp = sel + (lane & 3) * selw + 64 + (lane & 3) - lane;  // + s: column s - lane, aligned
-    const int nch = (ncols + 127 + 63) / 64;
-    for (int k = k0; k < nch && k < k1; ++k) {
-        if (k >= kSwPk2SlotsA && !sw_pk_wait(c, &misc[6], k + 1 - kSwPk2SlotsA)) return false;
-        if (k >= kSwPk2SlotsB && !sw_pk_wait(c, &misc[9], k + 1 - kSwPk2SlotsB)) return false;
-        uint4 *da = ringA + (size_t)((k % kSwPk2SlotsA) * 16) * 64 + lane;
-        uint4 *db = ringB + (size_t)((k % kSwPk2SlotsB) * 16) * 64 + lane;
-        const int *sp = selp + 64 * k;
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-            const int4 sv = *(const int4 *)(sp + 4 * g);
-            da[g * 64] = make_uint4(__builtin_amdgcn_perm(mhiA, mloA, (uint32_t)sv.x),
-                                    __builtin_amdgcn_perm(mhiA, mloA, (uint32_t)sv.y),
-                                    __builtin_amdgcn_perm(mhiA, mloA, (uint32_t)sv.z),
-                                    __builtin_amdgcn_perm(mhiA, mloA, (uint32_t)sv.w));
-            db[g * 64] = make_uint4(__builtin_amdgcn_perm(mhiB, mloB, (uint32_t)sv.x),
-                                    __builtin_amdgcn_perm(mhiB, mloB, (uint32_t)sv.y),
-                                    __builtin_amdgcn_perm(mhiB, mloB, (uint32_t)sv.z),
-                                    __builtin_amdgcn_perm(mhiB, mloB, (uint32_t)sv.w));
-        }
-        if (lane == 0) lds_flag_st(&misc[5], k + 1);
-    }
-    return true;
-}
-
-// One sweep wave of the two-sweep body (H = 0: A, rows 1..128; 1: B, rows
-// 129..256). top: the top row this wave's lane 0 reads (A: the tile's, staged
-// here; B: row 128, published by A into topB). A takes the tile's top row and
-// corner inputs, B writes the bottom row and the bottom-right corner; each
-// writes its half of the right column.
-template <int KX, int H>
-__device__ bool sw_pk2_tile(const SwCtx &c, const SwPkTile &T, int *top, int *topB, const uint4 *ring, int *misc,
-                            int *dummy) {
-    const int lane = lane_id();
-    const int ncols = T.ncols, R0 = T.R0, C0 = T.C0;
-    const int topw = sw_pk_topw(ncols);
-    const int xmax = ncols - 1;
-    constexpr int NQ = H ? 3 : 2;
-    int rowq[3];  // matrix rows: lo, hi, and (B) row R0 + 128 (its left value: lane 0's first diagonal)
-    rowq[0] = R0 + 1 + 128 * H + lane;
-    rowq[1] = rowq[0] + 64;
-    rowq[2] = R0 + 128;
-    const bool lglob = T.leftcol != nullptr;
-    const bool tin = !H && T.hin;
-    const sw_gran *lsrc = lglob ? T.leftcol : T.hout;
-    const sw_gran *hsrc = tin ? T.hin : T.hout;
-    sw_gran lg[3] = {0, 0, 0}, th_[KX], cg = 0;
-#pragma unroll
-    for (int k = 0; k < KX; ++k) th_[k] = 0;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t n = 0; tin || lglob || T.corner_src; ++n) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) lg[q] = ld_agent(&lsrc[lglob ? rowq[q] - R0 - 1 : 0]);
-        if (!H) {
-#pragma unroll
-            for (int k = 0; k < KX; ++k) {
-                const int x = lane + 64 * k;
-                th_[k] = ld_agent(&hsrc[tin ? (x < ncols ? x : xmax) : 0]);
-            }
-        }
-        cg = ld_agent(T.corner_src ? T.corner_src : T.hout);
-        bool ready = !T.corner_src || (cg >> 32) == 1ull;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) ready = ready && (!lglob || (lg[q] >> 32) == 1ull);
-        if (!H) {
-#pragma unroll
-            for (int k = 0; k < KX; ++k) ready = ready && (!tin || (th_[k] >> 32) == 1ull);
-        }
-        if (__ballot(!ready) == 0) break;
-        __builtin_amdgcn_s_sleep(1);
-        if ((n & 63) == 63) {
-            if (ld_agent(c.err)) return false;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * c.spin_ms) {
-                if (lane == 0) dev_error(c.err, kErrSpinTimeout);
-                return false;
-            }
-        }
-    }
-    const int cget = (int)(uint32_t)cg;
-    const int base = (T.corner_src ? cget : T.corner_val) + R0 + C0;  // G(R0, C0)
-    uint32_t l16[3] = {0, 0, 0};
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int lh = T.left_lds ? *((const lds_i32 *)T.left_lds + (rowq[q] - R0 - 1))
-                                  : (lglob ? (int)(uint32_t)lg[q] : -rowq[q]);
-        l16[q] = sw_f16_bits(lh + rowq[q] + C0 - base);
-    }
-    sw_h2 lr = sw_as_h2(l16[0] | (l16[1] << 16));
-    if (!H) {
-        // the top row as v (f16 in the low half), 0 past the tile
-#pragma unroll
-        for (int k = 0; k < KX + 4; ++k) {
-            const int x = lane + 64 * k;
-            if (x < topw) {
-                int v = 0;
-                if (k < KX && x < ncols)
-                    v = tin ? (int)(uint32_t)th_[k] + R0 + (C0 + 1 + x) - base
-                            : (T.top_lds ? *((const lds_i32 *)T.top_lds + x) + R0 + (C0 + 1 + x) - base : -base);
-                top[x] = (int)sw_f16_bits(v);
-            }
-        }
-        if (T.corner_lds) {
-            const int xl = ncols - 1;
-            if ((xl & 63) == lane) {
-                int hc = -(C0 + ncols);
-#pragma unroll
-                for (int k = 0; k < KX; ++k)
-                    if (k == (xl >> 6) && tin) hc = (int)(uint32_t)th_[k];
-                if (T.top_lds) hc = *((const lds_i32 *)T.top_lds + xl);
-                *T.corner_lds = hc;
-            }
-        }
-    } else {
-        // row 128 past the tile: 0 (A publishes the columns inside it)
-#pragma unroll
-        for (int k = 0; k < KX + 4; ++k) {
-            const int x = lane + 64 * k;
-            if (x >= ncols && x < topw) top[x] = 0;
-        }
-    }
-    // trace stamps: A as sw_pk_tile's, B's inputs / first chunk / sweep end at [13] / [14] / [15]
-    auto tstamp = [&](int k) {
-        const int kb = k == 8 ? 13 : k == 12 ? 14 : k == 10 ? 15 : -1;
-        if (HX_DAG_TRACE && T.trec && lane == 0 && (!H || kb >= 0)) T.trec[H ? kb : k] = __builtin_amdgcn_s_memrealtime();
-    };
-    tstamp(8);
-    const uint32_t selU = lane == 0 ? 0x05040100u : 0x07060504u;
-    // the up value of step -1: lane 0's low half the diagonal of its first
-    // cell (A: the corner, v = 0; B: row 128's left value)
-    sw_h2 upp = sw_as_h2(__builtin_amdgcn_perm((uint32_t)__builtin_amdgcn_mov_dpp((int)sw_as_u(lr), 0x13C, 0xf, 0xf, false),
-                                               H ? l16[2] : 0u, selU));
-    const int nsteps = ncols + 127;
-    const int Rb = R0 + kSwPkTh;
-    constexpr int kSlots = H ? kSwPk2SlotsB : kSwPk2SlotsA;
-    for (int s0 = 0, k = 0; s0 < nsteps; s0 += 64, ++k) {
-        if (!sw_pk_wait(c, &misc[5], k + 1)) return false;
-        if (H && !sw_pk_wait(c, &misc[10], s0 + 32 < ncols ? s0 + 32 : ncols)) return false;
-        if (k == 0) tstamp(12);
-        const uint4 *src = ring + (size_t)((k % kSlots) * 16) * 64 + lane;
-        uint32_t acc = 0;
-        constexpr int kPf = HX_SW_PK_PF;
-        int4 tq[kPf + 1];
-        uint4 rq[kPf + 1];
-        auto load_group = [&](int g) {
-            tq[g % (kPf + 1)] = *(const int4 *)(top + s0 + 4 * g);
-            rq[g % (kPf + 1)] = src[g * 64];
-        };
-#pragma unroll
-        for (int g = 0; g < kPf; ++g) load_group(g);
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-            if (H && g + kPf == 8 && !sw_pk_wait(c, &misc[10], s0 + 64 < ncols ? s0 + 64 : ncols)) return false;
-            if (g + kPf < 16) load_group(g + kPf);
-            const int4 tc = tq[g % (kPf + 1)];
-            const uint4 r = rq[g % (kPf + 1)];
-            const int tv[4] = {tc.x, tc.y, tc.z, tc.w};
-            const uint32_t sv[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const uint32_t rot = (uint32_t)__builtin_amdgcn_mov_dpp((int)sw_as_u(lr), 0x13C, 0xf, 0xf, false);
-                const sw_h2 up = sw_as_h2(__builtin_amdgcn_perm(rot, (uint32_t)tv[jj], selU));
-                const sw_h2 hn = __builtin_elementwise_maximum(__builtin_elementwise_maximum(lr, up), upp + sw_as_h2(sv[jj]));
-                if (jj & 1) {
-                    // lane 63's high halves of two steps as one word, shifted down a lane
-                    const uint32_t pair = __builtin_amdgcn_perm(sw_as_u(hn), sw_as_u(lr), 0x07060302u);
-                    acc = (uint32_t)__builtin_amdgcn_update_dpp((int)pair, (int)acc, 0x130, 0xf, 0xf, false);
-                }
-                upp = up;
-                lr = hn;
-            }
-            if (!H && (g & 3) == 3) {
-                // the quarter's 16 values of row 128 (lanes 56..63) for B
-                const int x0 = s0 + 4 * (g - 3) - 127 + 2 * (lane - 56);
-                const bool in0 = lane >= 56 && x0 >= 0 && x0 < ncols;
-                const bool in1 = lane >= 56 && x0 + 1 >= 0 && x0 + 1 < ncols;
-                *(in0 ? topB + x0 : dummy + lane) = (int)(acc & 0xFFFFu);
-                *(in1 ? topB + x0 + 1 : dummy + lane) = (int)(acc >> 16);
-                const int pubn = s0 + 4 * g + 4 - 127;  // columns below are final
-                if (pubn > 0 && lane == 63) lds_flag_st(&misc[10], pubn < ncols ? pubn : ncols);
-            }
-        }
-        if (lane == 0) lds_flag_st(&misc[H ? 9 : 6], k + 1);  // the chunk's ring slot is free
-        if (H) {
-            // lanes 32 + p hold steps s0 + 2p (low half) and s0 + 2p + 1 (high)
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int x = s0 + 2 * (lane - 32) + e - 127;  // the bottom row's column
-                if (lane >= 32 && x >= 0 && x < ncols) {
-                    const sw_h2 pv = sw_as_h2(acc);
-                    const int hb = (int)(float)(e ? pv.y : pv.x) + base - Rb - (C0 + 1 + x);
-                    st_agent(&T.hout[x], sw_granule(hb));
-                    if (x == ncols - 1) {
-                        if (T.corner_out) st_agent(T.corner_out, sw_granule(hb));
-                        if (T.corner_out_lds) *T.corner_out_lds = hb;
-                    }
-                }
-            }
-        }
-    }
-    tstamp(10);
-    // --- this wave's half of the right column
-    const int Cr = C0 + ncols;
-    int rv[2];
-    rv[0] = (int)(float)lr.x + base - rowq[0] - Cr;
-    rv[1] = (int)(float)lr.y + base - rowq[1] - Cr;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int k = rowq[q] - R0 - 1;
-        if (T.rightcol) st_agent(&T.rightcol[k], sw_granule(rv[q]));
-        if (T.rightcol_lds) T.rightcol_lds[k] = rv[q];
-    }
-    tstamp(11);
-    tstamp(9);
-    return true;
-}
-
 // The score wave, after staging the right neighbour (tile t + 1): poll its
 // top row (the up-right tile's bottom row) into LDS while this tile's sweep
 // runs (misc + kSwPkMisc + 256, then misc[8] = t + 1), so a kept neighbour
@@ -2046,118 +1800,6 @@ __global__ __launch_bounds__(192) void k_sw_dag_pk(SwCtx c, DagView v) {
     run_dag_group<SwDagPkKind>(c, v, nullptr);
 }
 
-// The promise DAG on the two-sweep body: workgroups of four waves, wave 0
-// sweep A (and the tickets), wave 1 the scores, wave 2 sweep B, wave 3
-// run_dag_group's helper. The tile task, its futures and puts are
-// SwDagPkKind's (smith_waterman.cpp:171-232); only the body differs.
-struct SwDagPk2Kind {
-    using Ctx = SwCtx;
-    static constexpr bool kSc1Payload = true;
-    static constexpr bool kTagged = true;
-    static constexpr bool kReserve = true;
-    __device__ static int *misc_of(const SwCtx &c) {
-        extern __shared__ __attribute__((aligned(16))) int sw_lds[];
-        return sw_lds + sw_pk2_lds_words(c.tw) - kSwPkMisc - 256 - kSwPkMaxTw;
-    }
-    // misc as SwDagPkKind's, and [9] chunks B has read, [10] columns of row
-    // 128 A has published (both reset between tiles); [4] is set by B
-    __device__ static bool run_group(const SwCtx &c, uint32_t t, const uint32_t *, int wave) {
-        extern __shared__ __attribute__((aligned(16))) int sw_lds[];
-        int *misc = misc_of(c);
-        uint4 *ringA = (uint4 *)sw_lds, *ringB = ringA + kSwPk2SlotsA * 16 * 64;
-        int *topA = sw_lds + kSwPk2RingU4 * 4, *topB = topA + sw_pk_topw(c.tw), *sel = topB + sw_pk_topw(c.tw);
-        int *right_keep = sel + 4 * sw_pk_selw(c.tw), *dummy = right_keep + 2 * kSwPkTh;
-        const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
-        if (wave == 3) return sw_pk_wait<true>(c, &misc[4], (int)t + 1);
-        if (wave == 1) {
-            int *tbl = misc + kSwPkMisc;
-            bool ok = true;
-            if (misc[7] != (int)t) {
-                auto first = [&]() { return sw_pk2_scores(c, c.tw, ringA, ringB, sel, tbl, misc, 0, 1); };
-                ok = c.tw <= 256 ? sw_pk_stage<4, decltype(first) &, true>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl, first)
-                                 : sw_pk_stage<8, decltype(first) &, true>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl, first);
-                if (ok) ok = sw_pk2_scores(c, c.tw, ringA, ringB, sel, tbl, misc, 1);
-            } else {
-                ok = sw_pk2_scores(c, c.tw, ringA, ringB, sel, tbl, misc);
-            }
-            if (!ok) return false;
-            const bool next = j + 1 < c.ntw;
-            auto none = []() { return true; };
-            if (next) {
-                if (c.tw <= 256) sw_pk_stage<4, decltype(none) &, true>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl, none);
-                else sw_pk_stage<8, decltype(none) &, true>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl, none);
-            }
-            if (lane_id() == 0) misc[7] = next ? (int)t + 1 : -1;
-            // the right neighbour's top row into LDS (as SwDagPkKind), once A
-            // has taken this tile's
-            if (next && i > 0 && sw_pk_wait(c, &misc[6], 1)) sw_pk_prefetch_top(c, t, misc);
-            return true;
-        }
-        const bool from_lds = j > 0 && misc[0] == (int)t - 1;
-        SwPkTile T;
-        T.R0 = i * kSwPkTh;
-        T.C0 = j * c.tw;
-        T.ncols = c.tw;
-        T.corner_src = (T.R0 == 0 || j == 0 || from_lds) ? nullptr : &c.gcorner[t - (uint32_t)c.ntw - 1];
-        T.corner_val = T.R0 == 0 ? -T.C0 : (j == 0 ? -T.R0 : (from_lds ? misc[1 + ((t - 1) & 1)] : 0));
-        T.hin = i > 0 ? c.gbot + (size_t)(t - (uint32_t)c.ntw) * c.tw : nullptr;
-        T.top_lds = (i > 0 && from_lds && misc[8] == (int)t) ? misc + kSwPkMisc + 256 : nullptr;
-        if (T.top_lds) T.hin = nullptr;
-        T.left_lds = j > 0 && from_lds ? right_keep + ((t - 1) & 1) * kSwPkTh : nullptr;
-        T.leftcol = j > 0 && !from_lds ? c.gright + (size_t)(t - 1) * kSwPkTh : nullptr;
-        T.hout = c.gbot + (size_t)t * c.tw;
-        T.rightcol = c.gright + (size_t)t * kSwPkTh;
-        T.rightcol_lds = right_keep + (t & 1) * kSwPkTh;
-        T.corner_out = c.gcorner + t;
-        T.corner_out_lds = &misc[3];
-        T.corner_lds = &misc[1 + (t & 1)];
-        T.trec = HX_DAG_TRACE && c.dtrace ? c.dtrace + (size_t)t * kDagTraceWords : nullptr;
-        if (wave == 0)
-            return c.tw <= 256 ? sw_pk2_tile<4, 0>(c, T, topA, topB, ringA, misc, dummy)
-                               : sw_pk2_tile<8, 0>(c, T, topA, topB, ringA, misc, dummy);
-        const bool ok = c.tw <= 256 ? sw_pk2_tile<4, 1>(c, T, topB, topB, ringB, misc, dummy)
-                                    : sw_pk2_tile<8, 1>(c, T, topB, topB, ringB, misc, dummy);
-        if (ok && lane_id() == 0) lds_flag_st(&misc[4], (int)t + 1);
-        return ok;
-    }
-    __device__ static void after_body(const SwCtx &c, uint32_t t) {
-        if (threadIdx.x == 0) {
-            int *misc = misc_of(c);
-            misc[0] = (int)t;
-            misc[5] = 0;
-            misc[6] = 0;
-            misc[9] = 0;
-            misc[10] = 0;
-        }
-    }
-    static constexpr int kPutN = 3;
-    __device__ static void promises(const SwCtx &, uint32_t t, uint32_t (&p)[3]) {
-        p[0] = 3u * t + 0u;
-        p[1] = 3u * t + 1u;
-        p[2] = 3u * t + 2u;
-    }
-    __device__ static void datums(const SwCtx &c, uint32_t, unsigned long long (&d)[3]) {
-        d[0] = 0ull;
-        d[1] = 0ull;
-        d[2] = (unsigned long long)(uint32_t)misc_of(c)[3];
-    }
-};
-
-__global__ __launch_bounds__(256) void k_sw_dag_pk2(SwCtx c, DagView v) {
-    int *misc = SwDagPk2Kind::misc_of(c);
-    if (threadIdx.x == 0) {
-        misc[0] = -2;
-        misc[4] = 0;
-        misc[5] = 0;
-        misc[6] = 0;
-        misc[7] = -1;
-        misc[8] = -1;
-        misc[9] = 0;
-        misc[10] = 0;
-    }
-    run_dag_group<SwDagPk2Kind>(c, v, nullptr);
-}
-
 __global__ void k_sw_init(uint32_t *deps, uint32_t *ready, int ntw, int nth) {
     const uint32_t n = (uint32_t)(ntw * nth);
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
@@ -2211,9 +1853,9 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     const bool band = rows && band_shape && !(sched && !strcmp(sched, "rows1"));
     // the promise DAG's 256-row tiles at most 512 wide: the packed-half body,
     // tagged outputs (HCLIB_HIP_SW_PK=0: the band forms)
+    // (a two-sweep-wave body was exact but slower, 7.95 vs 6.56 ms, and was
+    // removed in round 5: DESIGN.md §11)
     const bool pk = dag && th == kSwPkTh && tw <= kSwPkMaxTw && env_int("HCLIB_HIP_SW_PK", 1) != 0;
-    // ... with two sweep waves per tile (HCLIB_HIP_SW_PK=2)
-    const bool pk2 = pk && env_int("HCLIB_HIP_SW_PK", 1) == 2;
     const size_t nt = ntw * nth;
     const size_t b_s1 = ntw * tw, b_s2 = nth * th;
     const size_t b_bot = (rows || pk) ? 0 : nt * tw * 4, b_right = (rows || pk) ? 0 : nt * th * 4, b_c = nt * 4,
@@ -2316,12 +1958,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
                                                   : (wg ? env_int("HCLIB_HIP_SW_DAG_WGS_PER_CU", 1) : wpc),
                                       c.spin_ms, &L)))
             return fail(rc);
-        if (pk && pk2) {
-            const size_t plds = sw_pk2_lds_bytes(tw);
-            c.dtrace = ((const DagView *)L.view)->trace;
-            (void)hipFuncSetAttribute((const void *)k_sw_dag_pk2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
-            hipLaunchKernelGGL(k_sw_dag_pk2, dim3(L.grid), dim3(256), plds, m.stream, c, *(const DagView *)L.view);
-        } else if (pk) {
+        if (pk) {
             const size_t plds = sw_pk_lds_bytes(tw);
             c.dtrace = ((const DagView *)L.view)->trace;
             if (plds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_pk,

@@ -618,6 +618,17 @@ extern "C" int hclib_hip_uts_bucket_check(const hclib_hip_uts_params_t *params, 
     return bad;
 }
 
+static thread_local hclib_hip_uts_launch_t g_last_launch{-1, 0, 0, 0, 0, 0, 0, 0, 0};
+
+extern "C" int hclib_hip_uts_last_launch(hclib_hip_uts_launch_t *out) {
+    if (!out) {
+        set_error("hclib_hip_uts_last_launch: null output");
+        return HCLIB_HIP_EINVAL;
+    }
+    *out = g_last_launch;
+    return g_last_launch.mode < 0 ? HCLIB_HIP_EINVAL : HCLIB_HIP_OK;
+}
+
 extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int shard, int nshards,
                                     int split_depth, hclib_hip_uts_result_t *result,
                                     uint64_t *level_hist, int max_levels) {
@@ -766,7 +777,6 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // (fixed-shape GEO trees on 512-item rings every 64: T1XL 51.5 -> 49.9 ms,
     // T1L even, T2L slower; profiles/r02/geo_knobs.log)
     cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", geo_fixed && ring_used >= 512 ? 64 : 32);
-    cfg.hunger_fast = (uint32_t)env_int("HCLIB_HIP_HUNGER_FAST", 0);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
     cfg.backoff = (uint32_t)env_int("HCLIB_HIP_BACKOFF", 16);
     cfg.defer = (uint32_t)env_int("HCLIB_HIP_DEFER", 1);
@@ -774,9 +784,6 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // whose ring fits two batches' pushes: the fixed-shape GEO trees on
     // 512-item rings)
     cfg.dual = (uint32_t)env_int("HCLIB_HIP_UTS_DUAL", 1);
-    cfg.spill_lo_hungry = (uint32_t)env_int("HCLIB_HIP_SPILL_LO_HUNGRY", 0);
-    cfg.ramp_chunk = (uint32_t)env_int("HCLIB_HIP_RAMP_CHUNK", 0);
-    cfg.spread = (uint32_t)env_int("HCLIB_HIP_SPREAD", 0);
     // breadth-first seeding (hx_sched.h seed_levels) for fixed-shape GEO
     // trees: the grid expands the top levels together and shares the level
     // that reaches HCLIB_HIP_SEED_PER_WAVE slots per wave out evenly, instead
@@ -835,6 +842,16 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         if (grid % wpg) wpg = 1;
         if (wpg == 2) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 2> : k_uts_search<kUtsBin, 0, 1024, false, 2>;
         if (wpg == 4) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 4> : k_uts_search<kUtsBin, 0, 1024, false, 4>;
+    }
+    {
+        int ring_k = mode == kUtsBin ? 1024 : 512;
+        if (mode == kUtsGeoFixed && !feat && !global) {
+            const int ring = env_int("HCLIB_HIP_UTS_RING", ring_default);
+            if (ring == 256 || ring == 1024) ring_k = ring;
+        }
+        g_last_launch = hclib_hip_uts_launch_t{mode, trace ? 2 : (feat || global ? 1 : 0), wpg, grid, ring_k,
+                                               seed.target ? 1 : 0, (int)seed.target, (int)cfg.spill_lo,
+                                               grid / (m.num_cus > 0 ? m.num_cus : 1)};
     }
     HX_TRY(check_resident((const void *)kern, grid / wpg, 64 * wpg, 0, "hclib_hip_uts_search"));
     hipLaunchKernelGGL(kern, dim3(grid / wpg), dim3(64 * wpg), 0, m.stream, ctx, pool, m.globals, cfg);

@@ -268,6 +268,16 @@ int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int shard, int ns
                          int split_depth, hclib_hip_uts_result_t *result, uint64_t *level_hist,
                          int max_levels);
 
+/* The launch shape hclib_hip_uts_search chose for its last search on this
+ * thread's module (diagnostic: tests pin the bench's exact configuration).
+ * mode: 0 rule tables in global memory, 1 in LDS, 2 BIN, 3 fixed-shape GEO;
+ * feat: 0 the plain kernel, 1 sharding / per-level counts, 2 depth trace;
+ * seeded: breadth-first seeding of the top levels (seed_target slots). */
+typedef struct {
+    int mode, feat, workers_per_group, grid, ring, seeded, seed_target, spill_lo, waves_per_cu;
+} hclib_hip_uts_launch_t;
+int hclib_hip_uts_last_launch(hclib_hip_uts_launch_t *out);
+
 /* Cross-GPU work sharing for sharded searches (one process per GPU;
  * SURVEY 8e items 2-3; the reference's distributed UTS moves work between
  * ranks, test/performance-regression/full-apps/uts/uts_hclib_shmem_opt.cpp

@@ -267,7 +267,13 @@ __device__ __forceinline__ uint32_t finish_promote(const FinishArena &a, LocalSc
     if (lane == lead) base = add_agent(a.next, tot);
     base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
     if (base + tot > a.cap) {
-        if (lane == lead) dev_error(err, kErrArena);
+        // out of arena (reported; the launch fails): close this round so a
+        // later promotion never takes its stale marks for its own
+        if (lane == lead) {
+            dev_error(err, kErrArena);
+            ls.epoch = ep;
+        }
+        asm volatile("" ::: "memory");
         return kScopeRoot;
     }
     uint32_t h = base + off;
@@ -330,14 +336,11 @@ __device__ __forceinline__ uint32_t finish_open_local(const FinishArena &a, Loca
 // in lock step: per step one LDS atomic (its meta read beside it) per lane
 // still climbing; slots freed in a step go onto the free list by ballot rank
 // (no returning atomic), the list's length kept in a scalar until the end.
-// max_levels / pend: a lane completes at most max_levels scopes here; one
-// that is last out of a further scope stops there and names it in *pend.
 template <int N, class Cont>
 __device__ __forceinline__ uint32_t finish_check_out_local(const FinishArena &a, LocalScopes<N> &ls, uint32_t s,
                                                            unsigned long long value, Cont &&cont,
-                                                           FinishInFlight *q = nullptr, uint32_t *steps = nullptr,
-                                                           uint32_t max_levels = ~0u, uint32_t *pend = nullptr) {
-    uint32_t ran = 0;
+                                                           FinishInFlight *q = nullptr, uint32_t *steps = nullptr) {
+    uint32_t ran = 0;  // scopes this lane completed (joins)
     unsigned long long v = value & kScopeSumMask;
     uint32_t nf = (uint32_t)__builtin_amdgcn_readfirstlane((int)ls.nfree);
     bool go = true, hbm = false, freed_any = false;
@@ -375,11 +378,6 @@ __device__ __forceinline__ uint32_t finish_check_out_local(const FinishArena &a,
                         }
                         if ((old >> 56) != 1) {
                             go = false;
-                        } else if (ran >= max_levels) {
-                            // climbed far enough: the caller continues from the
-                            // completed scope s later (its sum stays in its word)
-                            go = false;
-                            if (pend) *pend = s;
                         } else {
                             freeing = true;
                             v = cont(meta.y, (old + add) & kScopeSumMask) & kScopeSumMask;

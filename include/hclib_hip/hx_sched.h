@@ -254,18 +254,10 @@ struct SchedConfig {
                          // (no ring push / pop) while they fit one batch and no hungry
                          // wave could take them (see run_worker); 2 also runs narrow
                          // frontiers in a tight carry-to-carry loop, 1 does not
-    uint32_t hunger_fast = 0;  // batches between hunger reads while many waves are
-                               // hungry (0: (hunger + 3) / 4)
     uint32_t defer = 1;  // a hunger spill's chunk is published after the next batch body
-                         // (PendingChunk) instead of behind a store round trip; 2: only
-                         // while at most 1/8 of the waves are hungry
+                         // (PendingChunk) instead of behind a store round trip
     uint32_t dual = 1;   // kinds with process2 (KindDual): a wave holding more than 64
                          // items runs TWO per lane per batch, their bodies interleaved
-    uint32_t spill_lo_hungry = 0;  // spill_lo while more than 1/8 of the waves are hungry
-                                   // (ramp-up, the tail of a search); 0: spill_lo always
-    uint32_t spread = 0;           // deques a wave's chunks go to (see the spill loop)
-    uint32_t ramp_chunk = 0;       // items per chunk given away while more than 1/8 of the
-                                   // waves are hungry (more, smaller gifts); 0: pool.chunk
 };
 
 // Kind concept:
@@ -817,13 +809,6 @@ __device__ uint32_t global_dequeue(const GlobalView &gv, uint32_t words_per_chun
     }
     vm_drain();
     return n;
-}
-
-// the give-away threshold: spill_lo, or spill_lo_hungry while more than an
-// eighth of the waves are hungry (a ramp-up, the tail of a search: work then
-// is worth more on an idle wave than deeper in this one's ring)
-__device__ __forceinline__ uint32_t spill_lo_now(const SchedConfig &cfg, uint32_t hungry) {
-    return (cfg.spill_lo_hungry && hungry * 8u > cfg.nwaves) ? cfg.spill_lo_hungry : cfg.spill_lo;
 }
 
 __device__ __forceinline__ uint32_t xorshift(uint32_t &s) {
@@ -1775,8 +1760,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 // many hungry waves (ramp-up, a narrowing tree): read again
                 // soon; otherwise every cfg.hunger batches
                 const uint32_t hg = cfg.nwaves > outst_cur ? cfg.nwaves - outst_cur : 0u;
-                const uint32_t fast = cfg.hunger_fast ? cfg.hunger_fast : (cfg.hunger + 3u) / 4u;
-                hunger_in = hg * 8u > cfg.nwaves ? fast : cfg.hunger;
+                hunger_in = hg * 8u > cfg.nwaves ? (cfg.hunger + 3u) / 4u : cfg.hunger;
             }
             --hunger_in;
             outst = outst_cur;
@@ -1937,7 +1921,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         {
             const uint32_t hungry0 = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
             if (cfg.carry && uniform && tout > 0 && tout <= (uint32_t)kWaveSize &&
-                !(hungry0 > 0 && (top - bot) + tout >= spill_lo_now(cfg, hungry0))) {
+                !(hungry0 > 0 && (top - bot) + tout >= cfg.spill_lo)) {
                 if constexpr (WaveStack<Kind, CAP>::kCarryLds) carry_lds<TW>(st.cscr, spawn, mu, child, ctmpl, ck);
                 else carry_permute<TW>(spawn, mu, nch, child, ctmpl, ck);
                 carry = tout;
@@ -1993,10 +1977,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         // ---- give the oldest items to hungry waves, or relieve a full ring
         uint32_t sz = top - bot;
         uint32_t hungry = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
-        const uint32_t lo = spill_lo_now(cfg, hungry);
+        const uint32_t lo = cfg.spill_lo;
         if (sz > cfg.spill_hi || (hungry > 0 && sz >= lo)) {
             const unsigned long long ts = __builtin_amdgcn_s_memtime();
-            const uint32_t cmax = (cfg.ramp_chunk && hungry * 8u > cfg.nwaves) ? cfg.ramp_chunk : pool.chunk;
+            const uint32_t cmax = pool.chunk;
             while (sz > cfg.spill_hi || (hungry > 0 && sz >= lo)) {
                 uint32_t n = (sz + 1) / 2;
                 if (n > cmax) n = cmax;
@@ -2013,22 +1997,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     }
                 }
                 if (!ok) publish_pending<Kind, CAP>(pool, g, pend);  // one deferred chunk at a time
-                // where the chunk goes: cfg.spread 0 = the home deque first, then the
-                // XCD's others; 1 = the XCD's deques in turn (chunk after chunk), so
-                // idle waves probing their own home deques find work without all
-                // converging on one deque's head; 2 = as 1, and over every XCD's
-                // deques while more than 1/8 of the waves are hungry (a ramp-up
-                // from one root reaches the other XCDs' idle waves at once)
-                // (cfg.defer 2: publish at once while many waves are hungry — a
-                // consumer that claims the ticket waits for the publish, on
-                // average a whole producer batch, profiles/r04 probe stats)
-                const bool defer_now = cfg.defer == 1 || (cfg.defer == 2 && hungry * 8u <= cfg.nwaves);
-                const uint32_t rot = cfg.spread ? npush : 0u;
-                const bool wide = cfg.spread > 1 && hungry * 8u > cfg.nwaves;
+                // where the chunk goes: the home deque first, then the XCD's others
                 for (uint32_t a = 0; a < qpx && !ok; ++a) {
-                    const uint32_t q = wide ? (home + (rot + a) * (qpx + 1u)) % pool.nq
-                                            : xcc * qpx + (home - xcc * qpx + rot + a) % qpx;
-                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, q, st, bot, n, occ, defer_now ? &pend : nullptr);
+                    const uint32_t q = xcc * qpx + (home - xcc * qpx + a) % qpx;
+                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, q, st, bot, n, occ, cfg.defer ? &pend : nullptr);
                 }
                 if (!ok) break;  // deques full: keep the items (the ring still has room)
                 ++npush;

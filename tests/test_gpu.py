@@ -148,10 +148,25 @@ def test_uts_small_trees_bit_exact(golden, name):
         assert r["levels"] == g["levels"][name]
 
 
-def test_uts_repeatable():
-    a = H.uts("-t 1 -a 3 -d 10 -b 4 -r 19")
-    b = H.uts("-t 1 -a 3 -d 10 -b 4 -r 19")
-    assert (a["nodes"], a["leaves"], a["max_depth"]) == (b["nodes"], b["leaves"], b["max_depth"])
+@pytest.mark.parametrize("name,want", [
+    # bench.py's T1 launch: the plain kernel (no per-level counts), fixed-shape
+    # GEO, breadth-first seeded, 512-item rings, 4 waves per CU
+    ("T1", {"mode": "geo_fixed", "feat": 0, "seeded": 1, "ring": 512, "waves_per_cu": 4,
+            "workers_per_group": 1}),
+    # BIN: two worker waves per workgroup (LDS inboxes), the plain kernel
+    ("T3", {"mode": "bin", "feat": 0, "seeded": 0, "ring": 1024, "workers_per_group": 2}),
+])
+def test_uts_bench_launch_shape_bit_exact(golden, name, want):
+    """The exact launch the bench runs (no max_levels: FEAT = 0, the kernel
+    test_uts_small_trees_bit_exact does not reach) against the published
+    counts (test/uts/sample_trees.sh:17-18, 26-27), and the launch shape
+    itself (hclib_hip_uts_last_launch)."""
+    pub = golden("uts_goldens.json")["published"][name]
+    r = H.uts(pub["args"])
+    assert (r["nodes"], r["leaves"], r["max_depth"]) == (pub["nodes"], pub["leaves"], pub["depth"])
+    shape = H.uts_last_launch()
+    for k, v in want.items():
+        assert shape[k] == v, (name, k, shape)
 
 
 @pytest.mark.parametrize("name", ["T3L", "T1L"])
@@ -261,26 +276,24 @@ def test_persistent_launch_that_cannot_be_resident_fails_fast(monkeypatch):
     assert H.fib(20)[0] == 6765
 
 
-@pytest.mark.parametrize("mode", [{"HCLIB_HIP_FIB_LOCAL": "0"},
-                                  {"HCLIB_HIP_FIB_CLIMB": "1073741824", "HCLIB_HIP_FIB_DEFER": "0"},
-                                  {"HCLIB_HIP_FIB_CLIMB": "1073741824", "HCLIB_HIP_FIB_DEFER": "1"},
-                                  {"HCLIB_HIP_FIB_CLIMB": "0", "HCLIB_HIP_FIB_DEFER": "0"},
-                                  {"HCLIB_HIP_FIB_CLIMB": "0", "HCLIB_HIP_FIB_DEFER": "1"},
-                                  {"HCLIB_HIP_FIB_CLIMB": "1", "HCLIB_HIP_FIB_DEFER": "1"},
-                                  {"HCLIB_HIP_FIB_CLIMB": "3", "HCLIB_HIP_FIB_DEFER": "1"},
+@pytest.mark.parametrize("mode", [{"HCLIB_HIP_FIB_LOCAL": "0"}, {},
                                   {"HCLIB_HIP_FIB_SEED": "0"}, {"HCLIB_HIP_FIB_SEED": "1"},
-                                  {"HCLIB_HIP_FIB_SEED": "4", "HCLIB_HIP_WAVES_PER_CU": "2"}])
+                                  {"HCLIB_HIP_FIB_SEED": "4", "HCLIB_HIP_WAVES_PER_CU": "2"},
+                                  {"HCLIB_HIP_FIB_BLOCKS": "0"},
+                                  {"HCLIB_HIP_FIB_BLOCKS": "0", "HCLIB_HIP_GRID": "300"}])
 def test_fib_finish_scope_modes(mode, monkeypatch):
     """Every join mode gives the same value, tasks and joins: HBM scopes only;
-    LDS scopes (hx_finish.h LocalScopes) climbing inline (unbounded, or
-    HCLIB_HIP_FIB_CLIMB levels and then as a continuation item) or one level
-    per task (continuation items only), with HBM check-outs waited for or
-    resolved a batch later (finish_issue / finish_resolve); breadth-first
-    seeding of the call tree's top levels (HCLIB_HIP_FIB_SEED items per
-    worker); fib(25) and fib(30)."""
+    LDS scopes (hx_finish.h LocalScopes, the default) climbing inline with
+    their HBM check-outs resolved a batch later (finish_issue /
+    finish_resolve); breadth-first seeding of the call tree's top levels
+    (HCLIB_HIP_FIB_SEED items per worker); scope ids taken one at a time
+    (HCLIB_HIP_FIB_BLOCKS=0), also on a grid whose seeding reservation is
+    not a power of two: the arena holds the seeding's whole reservation
+    (round-4 advisor). fib(10) (a 90-id call tree, smaller than the
+    reservation), fib(25) and fib(30)."""
     for k, v in mode.items():
         monkeypatch.setenv(k, v)
-    for n, want, calls in [(25, 75025, 242785), (30, 832040, 2692537)]:
+    for n, want, calls in [(10, 55, 177), (25, 75025, 242785), (30, 832040, 2692537)]:
         v, st = H.fib(n)
         assert v == want, (mode, n)
         assert st["tasks"] == calls and st["joins"] == (calls - 1) // 2, (mode, n, st)
@@ -330,10 +343,10 @@ def test_sw_64k_golden_on_generic_promise_dag(golden, monkeypatch):
     assert st["tiles"] == 65536
 
 
-@pytest.mark.parametrize("pk", ["1", "2"])
+@pytest.mark.parametrize("pk", ["1", "0"])
 def test_sw_64k_golden_on_packed_bodies(golden, pk, monkeypatch):
-    """SW-64K on the promise DAG with the one-sweep-wave (1) and the
-    two-sweep-wave (2) packed tile bodies: 128772."""
+    """SW-64K on the promise DAG with the packed one-sweep-wave tile body (1)
+    and the int32 band body (0): 128772."""
     monkeypatch.setenv("HCLIB_HIP_SW_SCHED", "dag")
     monkeypatch.setenv("HCLIB_HIP_SW_PK", pk)
     s1, s2 = _sw_inputs("huge")
@@ -363,9 +376,6 @@ def test_sw_dag_packed_half_tiles(tw, monkeypatch):
         assert score == want and st["tiles"] == (n1 // tw) * 3, (tw, score, want)
         monkeypatch.setenv("HCLIB_HIP_SW_PK", "0")
         assert H.sw(a, b, tw, 256)[0] == want
-        # the two-sweep-wave body (sw_pk2_tile)
-        monkeypatch.setenv("HCLIB_HIP_SW_PK", "2")
-        assert H.sw(a, b, tw, 256)[0] == want, (tw, "pk2")
         monkeypatch.delenv("HCLIB_HIP_SW_PK")
 
 
