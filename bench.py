@@ -198,23 +198,47 @@ def measure_triad(H, reps=20, n=1 << 28, sync=None):
 
 def measure_atomics(H, fib_stats):
     """L2 atomic throughput of the fib megakernel (BASELINE north_star: the
-    fraction of peak L2 atomic throughput). Algorithmic atomics: one
-    returning 64-bit fetch-add per task check-out (tasks - 1; the root's
-    result is a store), the reference's check_out_finish
-    (src/hclib-runtime.c:431-446). Peak: the same access shape saturated by
-    hclib_hip_atomic_calibrate (every lane, random 16-B records), measured
-    here in the same process; the hot-word and coalesced shapes are
-    reported beside it."""
+    fraction of peak L2 atomic throughput). Two figures, kept apart:
+    * algorithmic: one check-out per task (tasks - 1; the root's result is a
+      store), the reference's check_out_finish (src/hclib-runtime.c:431-446),
+      as a rate over this run's kernel time;
+    * counted: the L2 atomic requests rocprofv3 counted per fib(30) launch
+      (TCC_ATOMIC_sum, profiles/atomics_pmc.json from
+      scripts/pmc_atomics_r05.sh) over this run's kernel time, against the
+      scattered-returning peak measured here (hclib_hip_atomic_calibrate:
+      every lane its own random 16-B record). Most check-outs resolve in the
+      wave's LDS finish scopes (hx_finish.h LocalScopes) and never reach L2:
+      `lds_checkout_share` says how many."""
     scatter, _ = H.atomic_calibrate(H.ATOMIC_SCATTER_RET64, 256)
     hot, _ = H.atomic_calibrate(H.ATOMIC_HOT_WORD, 256)
     coal, _ = H.atomic_calibrate(H.ATOMIC_COALESCED32, 256)
     ops = fib_stats["tasks"] - 1
-    achieved = ops / (fib_stats["kernel_ms"] * 1e-3) / 1e6
-    return {"kernel": "k_fib (fib(30) join check-outs)", "unit": "Mops/s",
-            "algorithmic_atomics_per_launch": ops, "achieved": achieved,
-            "peak": scatter, "frac": achieved / scatter,
-            "peak_shape": "returning 64-bit add, every lane its own random 16-B record (256 MiB)",
-            "hot_word_peak": hot, "coalesced32_peak": coal}
+    sec = fib_stats["kernel_ms"] * 1e-3
+    out = {"kernel": "k_fib (fib(30) join check-outs)", "unit": "Mops/s",
+           "algorithmic_atomics_per_launch": ops, "algorithmic_checkouts_per_s": ops / sec / 1e6,
+           "peak": scatter,
+           "peak_shape": "returning 64-bit add, every lane its own random 16-B record (256 MiB)",
+           "hot_word_peak": hot, "coalesced32_peak": coal}
+    pmc = None
+    p = os.path.join(ROOT, "profiles", "atomics_pmc.json")
+    if os.path.exists(p):
+        try:
+            pmc = json.load(open(p))
+        except Exception:  # noqa: BLE001
+            pmc = None
+    fib = (pmc or {}).get("fib30")
+    if fib:
+        counted = fib["counted_l2_atomics_per_launch"]
+        out.update({"counted_l2_atomics_per_launch": counted,
+                    "achieved": counted / sec / 1e6, "frac": counted / sec / 1e6 / scatter,
+                    "lds_checkout_share": fib.get("lds_checkout_share"),
+                    "l2_atomics_per_checkout": fib.get("l2_atomics_per_checkout"),
+                    "counted_source": "profiles/atomics_pmc.json (rocprofv3 --pmc TCC_ATOMIC_sum, "
+                                      "scripts/pmc_atomics_r05.sh)"})
+    else:
+        out.update({"achieved": None, "frac": None,
+                    "counted_source": "missing: profiles/atomics_pmc.json"})
+    return out
 
 
 def load_pmc_traffic():

@@ -219,11 +219,13 @@ struct UtsKind {
     }
 
     // everything after the spawn: counting, numChildren, the child template
+    // (F: the FEAT whose side paths run; the shard filter from F = 1 on)
+    template <int F = FEAT>
     __device__ static __forceinline__ int finish(const Ctx &c, Acc &acc, const uint32_t *t, const uint32_t *ch,
                                                  uint32_t *child, uint32_t *err, bool valid) {
         const int h1 = (int)t[5] + 1;
         bool counted = valid;
-        if (FEAT && c.nshards > 1) {
+        if (F && c.nshards > 1) {
             if (h1 == c.split && (ch[0] % (uint32_t)c.nshards) != (uint32_t)c.shard) return 0;
             if (h1 < c.split && c.shard != 0) counted = false;
         }
@@ -234,8 +236,8 @@ struct UtsKind {
         acc.nodes += counted ? 1u : 0u;
         acc.leaves += (counted && nc <= 0) ? 1u : 0u;
         acc.maxd = (counted && (uint32_t)h1 > acc.maxd) ? (uint32_t)h1 : acc.maxd;
-        if (FEAT == 1 && counted && c.hist && h1 < c.hist_levels) atomicAdd(&c.hist[h1], 1ull);
-        if (FEAT == 2 && c.hist) {
+        if (F == 1 && counted && c.hist && h1 < c.hist_levels) atomicAdd(&c.hist[h1], 1ull);
+        if (F == 2 && c.hist) {
             const uint32_t dm = wave_max(counted ? (uint32_t)h1 : 0u);
             if (dm > acc.trace_seen) {
                 acc.trace_seen = dm;
@@ -264,6 +266,19 @@ struct UtsKind {
         rng_spawn_dev(t, k, ch);
         for (int g = 1; g < c.gran; ++g) rng_spawn_dev(t, k, ch);  // -g: repeated spawns
         return finish(c, acc, t, ch, child, err, valid);
+    }
+
+    // the breadth-first seeding's slots (hx_sched.h seed_levels) run with the
+    // shard filter and the top levels' counting rule whatever FEAT is: a
+    // seeded shard's levels reach past its split depth (the host launches
+    // FEAT = 0 only then), so its work-stealing loop, the plain kernel of a
+    // whole-tree search, never meets a node at or above the split
+    __device__ static int seed_process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k, uint32_t *child,
+                                       uint32_t *err, bool valid) {
+        uint32_t ch[5];
+        rng_spawn_dev(t, k, ch);
+        for (int g = 1; g < c.gran; ++g) rng_spawn_dev(t, k, ch);
+        return finish<FEAT == 0 ? 1 : FEAT>(c, acc, t, ch, child, err, valid);
     }
 
     // two nodes per lane (dual batches of the megakernel, hx_sched.h): the two
@@ -618,6 +633,9 @@ extern "C" int hclib_hip_uts_bucket_check(const hclib_hip_uts_params_t *params, 
     return bad;
 }
 
+#ifndef HX_UTS_SHARD_FILTER_IN_LOOP
+#define HX_UTS_SHARD_FILTER_IN_LOOP 0
+#endif
 static thread_local hclib_hip_uts_launch_t g_last_launch{-1, 0, 0, 0, 0, 0, 0, 0, 0};
 
 extern "C" int hclib_hip_uts_last_launch(hclib_hip_uts_launch_t *out) {
@@ -802,7 +820,14 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     }
     HX_TRY(reset_sched(pool, 1, global, (uint32_t)grid, seed.target ? &seed : nullptr));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
-    const bool feat = nshards > 1 || max_levels > 0;
+    // a sharded search whose seeding reaches past its split (every seeded
+    // fixed-shape shard with split < the seeding's level bound) filters its
+    // shard inside the seeding (UtsKind::seed_process) and then runs the
+    // plain kernel; otherwise the worker loop itself filters (FEAT = 1)
+    // (HX_UTS_SHARD_FILTER_IN_LOOP=1 builds the round-4 form for an A/B)
+    const bool seed_past_split = !HX_UTS_SHARD_FILTER_IN_LOOP && seed.target &&
+                                 split_depth < (int)seed.max_levels && split_depth + 1 < kSeedMaxLevels;
+    const bool feat = max_levels > 0 || (nshards > 1 && (global || !seed_past_split));
     if (bin) ctx.bin_thr = (uint32_t)T.rules[1].y;
     const int mode = bin ? kUtsBin : geo_fixed ? kUtsGeoFixed : (ctx.lds_tables ? kUtsRulesLds : kUtsRulesGlobal);
     typedef void (*uts_kernel_t)(UtsCtx, PoolView, SchedGlobals *, SchedConfig);

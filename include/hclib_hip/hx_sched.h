@@ -305,6 +305,23 @@ struct SchedConfig {
 #define HX_RESIDUAL_SPLIT_MIN 2
 #endif
 
+// a Kind's seeding slots run Kind::seed_process when it has one (UTS: the
+// shard filter at the split depth, which the seeding passes), else process
+template <class K, class = void>
+struct KindHasSeedProcess {
+    static constexpr bool value = false;
+};
+template <class K>
+struct KindHasSeedProcess<K, decltype((void)&K::seed_process)> {
+    static constexpr bool value = true;
+};
+template <class K>
+__device__ __forceinline__ int kind_seed_process(const typename K::Ctx &c, typename K::Acc &acc, const uint32_t *t,
+                                                 uint32_t k, uint32_t *child, uint32_t *err, bool valid) {
+    if constexpr (KindHasSeedProcess<K>::value) return K::seed_process(c, acc, t, k, child, err, valid);
+    else return K::process(c, acc, t, k, child, err, valid);
+}
+
 template <class K, class = void>
 struct KindPieces {
     static constexpr int value = 8;
@@ -1260,13 +1277,29 @@ __device__ __forceinline__ void wave_goes_idle(SchedGlobals *g, const GlobalView
 // slots of level d + 1 (one bump per wave). A level ends when every wave
 // that had a block has counted itself done (ctl line 2d + 1) — only the
 // participants touch the counters; everyone polls one line for a few
-// microseconds. Once a level holds at least `target` slots (or after
-// `max_levels`) every wave takes an equal share of it straight into its ring
-// and the work-stealing loop starts with every wave busy. ctl lines: [2d]
-// slots appended to level d, [2d + 1] waves done with level d, [2 L] the
-// root's level written (wave 0). The host sets `outstanding` to the wave
+// microseconds. The narrow top levels (at most kSoloCap slots) wave 0 runs
+// alone in its LDS ring, before any other wave is needed. Once a level holds
+// at least `target` slots (or after `max_levels`) every wave takes an equal
+// share of it straight into its ring and the work-stealing loop starts with
+// every wave busy. ctl lines: [2d + 1] one 64-bit word per grid-wide level d
+// {slots appended to level d + 1 (low half), participants done (high)},
+// then kSeedGoLines broadcast lines: word d < L the size + 1 of level d + 1,
+// words L / L + 1 the solo levels' result (size + 1, depth; wave 0). The host sets `outstanding` to the wave
 // count: every wave holds a unit until its share is taken.
 // Pure kinds only (the slots of a block run branch-free, as in a batch).
+// Ordering of the seeding's level hand-offs. Every word another wave reads
+// travels as an sc1 (device-coherent, write-through) store or load: the
+// slots (st_sc1_x4 / ld_sc1_x4x2), the counters and go lines (agent-scope
+// atomics). A producer drains its stores (s_waitcnt vmcnt(0)) before the
+// atomic or store that publishes them; the done add is acq_rel and the solo
+// result a release store. Full agent release / acquire fences around each
+// hand-off (L2 write-back and invalidate on every wave, every level:
+// HX_SEED_FENCES=1) cost T1 0.240-0.250 -> 0.256-0.267 ms and T1L 2.43 ->
+// 2.53 ms same-box (profiles/r05/ab_seedfence.log), so they are a build
+// option, not the default.
+#ifndef HX_SEED_FENCES
+#define HX_SEED_FENCES 0
+#endif
 template <class Kind, int CAP>
 __device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Acc &acc, SchedGlobals *g,
                                 WaveStack<Kind, CAP> &st, uint32_t gid, uint32_t nw, uint32_t spin_limit_ms,
@@ -1300,33 +1333,32 @@ __device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Ac
             __builtin_amdgcn_s_sleep(1);
         }
     };
-    // one block of 64 slots of level d (src) -> children as slots of level
-    // d + 1 (dst, count line cnt); false on an overflow (error recorded).
-    // Slots are 32 B {template, k, k + 1}, moved as 16-B sc1 accesses; the
-    // block's children are written flat (output o by lane o % 64, so every
-    // store instruction writes consecutive slots), the lane -> node map
-    // through the wave's (still empty) ring in LDS
-    auto run_block = [&](const uint32_t *src, uint32_t E, uint32_t b, uint32_t *dst, uint32_t *cnt) -> bool {
-        const uint32_t e = b * 64 + (uint32_t)lane;
-        const bool valid = e < E;
-        uint4 s0, s1;
-        ld_sc1_x4x2(src + (size_t)(valid ? e : 0u) * W, s0, s1);
-        const uint32_t tmpl[TW] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y};
+    // the lane -> node map of a block lives in ring entries [kScr, kScr + 64)
+    // (the ring is still empty; wave 0's solo levels use [0, 2 kSoloCap))
+    constexpr uint32_t kSoloCap = (uint32_t)(CAP - 64) / 2;
+    constexpr uint32_t kScr = 2 * kSoloCap;
+    static_assert(kSoloCap >= 64, "the solo levels need ring room");
+    // one block of 64 slots (template `tmpl`, child k, valid) -> the children
+    // of every node as slots of the next level, written flat to dst from
+    // slot `base` (output o by lane o % 64, so every store instruction writes
+    // consecutive slots) and, for outputs below kSoloCap, to the LDS level
+    // buffer at ring entry `lds_out` (~0u: none). Slots are 32 B {template,
+    // k, k + 1}, stored as 16-B sc1 accesses; base / count come from `alloc`
+    auto run_slots = [&](const uint32_t (&tmpl)[TW], uint32_t k, bool valid, uint32_t *dst, uint32_t lds_out,
+                         auto &&alloc) -> bool {
         uint32_t child[TW];
-        const int nc = Kind::process(ctx, acc, tmpl, s1.z, child, err, valid);
+        const int nc = kind_seed_process<Kind>(ctx, acc, tmpl, k, child, err, valid);
         ++nbatch;
         const uint32_t u = valid && nc > 0 ? (uint32_t)nc : 0u;
         n_exec += valid ? 1u : 0u;
         n_spawn += u;
         const int S = wave_scan_add((int)u);
         const uint32_t tot = (uint32_t)lane63(S), excl = (uint32_t)S - u;
-        uint32_t base = 0;
-        if (lane == 0 && tot) base = add_agent(cnt, tot);
-        st.t0[lane] = make_uint4(child[0], child[1], child[2], child[3]);
-        st.t1[lane] = make_uint2(child[4], child[5]);
-        st.d[lane] = make_uint2(excl, u);
+        const uint32_t base = alloc(tot);
+        st.t0[kScr + lane] = make_uint4(child[0], child[1], child[2], child[3]);
+        st.t1[kScr + lane] = make_uint2(child[4], child[5]);
+        st.d[kScr + lane] = make_uint2(excl, u);
         asm volatile("" ::: "memory");
-        base = lane0(base);
         if (base + tot > sd.cap) {  // the level buffer is sized by the host; never expected
             if (lane == 0) dev_error(err, kErrStackOverflow);
             return false;
@@ -1338,14 +1370,20 @@ __device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Ac
 #pragma unroll
                 for (int it = 0; it < 6; ++it) {
                     const int mid = (lo + hi + 1) >> 1;
-                    if (st.d[mid].x <= o) lo = mid;
+                    if (st.d[kScr + mid].x <= o) lo = mid;
                     else hi = mid - 1;
                 }
-                const uint32_t j = o - st.d[lo].x;
-                const uint2 t1 = st.t1[lo];
+                const uint32_t j = o - st.d[kScr + lo].x;
+                const uint4 t0 = st.t0[kScr + lo];
+                const uint2 t1 = st.t1[kScr + lo];
                 uint32_t *q = dst + (size_t)(base + o) * W;
-                st_sc1_x4(q, st.t0[lo]);
+                st_sc1_x4(q, t0);
                 st_sc1_x4(q + 4, make_uint4(t1.x, t1.y, j, j + 1));
+                if (lds_out != ~0u && base + o < kSoloCap) {
+                    st.t0[lds_out + base + o] = t0;
+                    st.t1[lds_out + base + o] = t1;
+                    st.d[lds_out + base + o] = make_uint2(j, j + 1);
+                }
             }
         }
         asm volatile("" ::: "memory");
@@ -1357,8 +1395,9 @@ __device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Ac
                (E >= sd.target && d >= (int)sd.min_levels);
     };
     // wave 0: the root's slots (level 0), and the narrow top levels on its
-    // own (no grid-wide round trips while a level fits a few batches)
-    constexpr uint32_t kSolo = 256;
+    // own, entirely in its ring (LDS) and registers: no round trip per
+    // block or level, the slots of every level also stored to HBM (stores
+    // only) for the grid-wide levels to read, drained once at the end
     uint32_t E = 0;
     int d = 0;
     if (gid == 0) {
@@ -1369,53 +1408,99 @@ __device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Ac
             uint32_t *q = buf(0) + (size_t)e * W;
             st_sc1_x4(q, make_uint4(tmpl[0], tmpl[1], tmpl[2], tmpl[3]));
             st_sc1_x4(q + 4, make_uint4(tmpl[4], tmpl[5], e, e + 1));
+            if (e < kSoloCap) {
+                st.t0[e] = make_uint4(tmpl[0], tmpl[1], tmpl[2], tmpl[3]);
+                st.t1[e] = make_uint2(tmpl[4], tmpl[5]);
+                st.d[e] = make_uint2(e, e + 1);
+            }
         }
-        vm_drain();
-        while (!stop(E, d) && E <= kSolo) {
-            for (uint32_t b = 0; b * 64 < E; ++b)
-                if (!run_block(buf(d), E, b, buf(d + 1), line(2 * (d + 1)))) break;
-            vm_drain();  // this wave's slot stores land before it reads them back
-            uint32_t e2 = 0;
-            if (lane == 0) e2 = ld_agent(line(2 * (d + 1)));
-            E = lane0(e2);
+        asm volatile("" ::: "memory");
+        uint32_t in = 0, out = kSoloCap;
+        bool ok = true;
+        while (ok && !stop(E, d) && E <= kSoloCap) {
+            uint32_t cnt = 0;
+            auto alloc = [&](uint32_t tot) {
+                const uint32_t b0 = cnt;
+                cnt += tot;
+                return b0;
+            };
+            for (uint32_t b = 0; b * 64 < E && ok; ++b) {
+                const uint32_t e = b * 64 + (uint32_t)lane;
+                const bool valid = e < E;
+                const uint32_t src = in + (valid ? e : 0u);
+                const uint4 a = st.t0[src];
+                const uint2 c = st.t1[src];
+                const uint32_t t[TW] = {a.x, a.y, a.z, a.w, c.x, c.y};
+                ok = run_slots(t, st.d[src].x, valid, buf(d + 1), out, alloc);
+            }
+            E = cnt;
             ++d;
+            const uint32_t x = in;
+            in = out;
+            out = x;
             tl.log(kTlSeed, (uint32_t)d);
         }
-        if (lane == 0) {
-            st_agent(line(2 * kSeedMaxLevels + 1), (uint32_t)d);
-            st_agent(line(2 * kSeedMaxLevels), E + 1);  // (release: the slots and d are drained above)
+        // every level's slots land before the result is published, on every
+        // broadcast line (1,023 waves polling one line made it a hot spot:
+        // the first grid-wide level took 20 us, timeline tl_t1_a)
+        if (HX_SEED_FENCES) release_agent();
+        for (uint32_t i = (uint32_t)lane; i < (uint32_t)kSeedGoLines; i += 64) {
+            // one 8-byte store {size + 1, depth}: a reader that sees the size sees the depth
+            unsigned long long *gl = (unsigned long long *)(line(2 * kSeedMaxLevels + 2 + (int)i) + kSeedMaxLevels);
+            st_agent(gl, (unsigned long long)(E + 1) | ((unsigned long long)(uint32_t)d << 32));
         }
         vm_drain();
+        if (!ok) return 0;
     }
-    if (!wait_ge(line(2 * kSeedMaxLevels), 1u)) return 0;
+    if (!wait_ge(go + kSeedMaxLevels, 1u)) return 0;
+    if (HX_SEED_FENCES) acquire_agent();
     if (lane == 0) {
-        E = ld_agent(line(2 * kSeedMaxLevels)) - 1u;
-        d = (int)ld_agent(line(2 * kSeedMaxLevels + 1));
+        const unsigned long long r = ld_agent((const unsigned long long *)(go + kSeedMaxLevels));
+        E = (uint32_t)r - 1u;
+        d = (int)(r >> 32);
     }
     E = lane0(E);
     d = (int)lane0((uint32_t)d);
-    // the wide levels: the grid's waves, 64 slots a block
+    // the wide levels: the grid's waves, 64 slots a block. Per level one
+    // 64-bit word (ctl line 2d + 1): low half the slots appended to level
+    // d + 1, high half the participants done; the participant whose done
+    // add completes the count reads the level's size from its own atomic
     for (; !stop(E, d); ++d) {
         const uint32_t nblk = (E + 63) / 64;
+        unsigned long long *word = (unsigned long long *)line(2 * d + 1);
+        auto alloc = [&](uint32_t tot) {
+            unsigned long long b0 = 0;
+            if (lane == 0 && tot) b0 = add_agent(word, (unsigned long long)tot);
+            return (uint32_t)lane0((uint32_t)b0);
+        };
         bool ok = true;
-        for (uint32_t b = gid; b < nblk && ok; b += nw) ok = run_block(buf(d), E, b, buf(d + 1), line(2 * (d + 1)));
+        for (uint32_t b = gid; b < nblk && ok; b += nw) {
+            const uint32_t e = b * 64 + (uint32_t)lane;
+            const bool valid = e < E;
+            uint4 s0, s1;
+            ld_sc1_x4x2(buf(d) + (size_t)(valid ? e : 0u) * W, s0, s1);
+            const uint32_t t[TW] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y};
+            ok = run_slots(t, s1.z, valid, buf(d + 1), ~0u, alloc);
+        }
         if (!ok) return 0;
         // participants count themselves done once their slots are drained; the
-        // last one tells every broadcast line (its count makes level d + 1 final)
+        // last one publishes the next level's size (+ 1) on every broadcast line
         const uint32_t P = nblk < nw ? nblk : nw;
         if (gid < P) {
             vm_drain();
-            uint32_t prev = 0;
-            if (lane == 0) prev = __hip_atomic_fetch_add(line(2 * d + 1), 1u, __ATOMIC_RELEASE, HX_AGENT);
-            if (lane0(prev) + 1u == P) {
-                const uint32_t e2 = lane == 0 ? ld_agent(line(2 * (d + 1))) : 0u;
-                const uint32_t e1 = lane0(e2) + 1u;  // (biased: 0 = not yet)
+            unsigned long long prev = 0;
+            if (lane == 0) prev = __hip_atomic_fetch_add(word, 1ull << 32, __ATOMIC_ACQ_REL, HX_AGENT);
+            const uint32_t done = lane0((uint32_t)(prev >> 32)) + 1u;
+            const uint32_t e1 = lane0((uint32_t)prev) + 1u;  // (biased: 0 = not yet)
+            if (done == P) {
                 // go line i holds, per level, the next level's size + 1 at word d
+                if (HX_SEED_FENCES) release_agent();
                 for (uint32_t i = (uint32_t)lane; i < (uint32_t)kSeedGoLines; i += 64)
                     st_agent(line(2 * kSeedMaxLevels + 2 + (int)i) + d, e1);
             }
         }
         if (!wait_ge(go + d, 1u)) return 0;
+        if (HX_SEED_FENCES) acquire_agent();
         uint32_t e2 = 0;
         if (lane == 0) e2 = ld_agent(go + d);
         E = lane0(e2) - 1u;

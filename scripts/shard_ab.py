@@ -1,0 +1,41 @@
+"""Same-box A/B of T1XL's 8-shard partition (split 7, bench.py's N = 8
+wide-tree leg) between library builds: per build, every shard's kernel time
+and the whole tree's, best of `reps` (development aid).
+    python scripts/shard_ab.py reps name=lib.so ..."""
+import json
+import os
+import subprocess
+import sys
+
+CHILD = r'''
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+import hclib_amd as H
+H.init(0)
+args = "-t 1 -a 3 -d 15 -b 4 -r 29"
+reps = int(sys.argv[2])
+shards = []
+for s in range(8):
+    best = None
+    for _ in range(reps):
+        r = H.uts(args, s, 8, 7)
+        best = r["kernel_ms"] if best is None else min(best, r["kernel_ms"])
+    shards.append((r["nodes"], round(best, 3)))
+assert sum(n for n, _ in shards) == 1635119272
+whole = min(H.uts(args)["kernel_ms"] for _ in range(reps))
+print(json.dumps({"shards": shards, "whole": round(whole, 3), "feat": H.uts_last_launch()["feat"]}))
+'''
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+reps = int(sys.argv[1])
+for a in sys.argv[2:]:
+    name, lib = a.split("=", 1)
+    env = dict(os.environ, HCLIB_AMD_LIB=lib)
+    p = subprocess.run([sys.executable, "-c", CHILD, root, str(reps)], env=env, capture_output=True, text=True,
+                       timeout=600)
+    if p.returncode:
+        print(name, "FAILED", p.stderr[-2000:], flush=True)
+        continue
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    slow = max(t for _, t in d["shards"])
+    print(f"{name}: whole {d['whole']} ms, shards {[t for _, t in d['shards']]} ms, slowest {slow}, "
+          f"projected efficiency {d['whole'] / (8 * slow):.3f}", flush=True)
