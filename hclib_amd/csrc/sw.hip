@@ -1488,6 +1488,7 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
     const sw_gran *lsrc = lglob ? T.leftcol : T.hout;
     const sw_gran *hsrc = T.hin ? T.hin : T.hout;
     sw_gran lg[4], th_[KX], cg = 0;
+    if (HX_DAG_TRACE && T.trec && lane == 0) T.trec[14] = __builtin_amdgcn_s_memrealtime();  // body entered
 #pragma unroll
     for (int q = 0; q < 4; ++q) lg[q] = 0;
 #pragma unroll
@@ -1517,6 +1518,12 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
                 return false;
             }
         }
+    }
+    if (HX_DAG_TRACE && T.trec && lane == 0) {
+        T.trec[15] = __builtin_amdgcn_s_memrealtime();  // inputs loaded
+        // [13]: where the inputs came from (scripts/sw_dag_trace.py)
+        T.trec[13] = (T.top_lds ? 1ull : 0ull) | (T.hin ? 2ull : 0ull) | (lglob ? 4ull : 0ull) |
+                     (T.corner_src ? 8ull : 0ull) | (T.left_lds ? 16ull : 0ull);
     }
     const int cget = (int)(uint32_t)cg;
     int lh[4];

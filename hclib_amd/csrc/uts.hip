@@ -814,9 +814,26 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         const int per_wave = env_int("HCLIB_HIP_SEED_PER_WAVE", uts_expected_nodes(*params) >= 3e7 ? 32 : 4);
         seed.target = (uint32_t)(grid * per_wave);
         seed.max_levels = (uint32_t)env_int("HCLIB_HIP_SEED_LEVELS", 20);
-        // a shard's share is only known past its split: level d holds the
-        // slots of depth d + 1, filtered when they run
-        seed.min_levels = nshards > 1 ? (uint32_t)split_depth : 0u;
+        // a shard's share is only known past its split (level d holds the
+        // slots of depth d + 1, filtered when they run), so the seeding goes
+        // on to the split — where the levels up to it fit the seeding's
+        // buffers (expected sizes n(d) = prod b_k): the unfiltered level
+        // (n(split) slots) within half the level buffer, and this shard's
+        // share of the level past it within a quarter of each wave's ring
+        // (hx_sched.h seed_levels: the buffer holds 8 x target + 65,536
+        // slots, a wave takes at most CAP / 2 items). Deeper splits seed
+        // only to the target and filter in the worker loop (FEAT = 1).
+        if (nshards > 1) {
+            double n_split = 1.0, n_next = 1.0;
+            for (int d = 0; d <= split_depth && d < 64; ++d) {
+                if (d < split_depth) n_split *= geo_bi(*params, d) > 0 ? geo_bi(*params, d) : 0.0;
+                n_next *= geo_bi(*params, d) > 0 ? geo_bi(*params, d) : 0.0;
+            }
+            const double cap = 8.0 * seed.target + 65536.0;
+            const bool fits = split_depth + 1 < kSeedMaxLevels && split_depth < (int)seed.max_levels &&
+                              n_split <= 0.5 * cap && n_next / nshards <= (double)grid * (512 / 8);
+            seed.min_levels = fits ? (uint32_t)split_depth : 0u;
+        }
     }
     HX_TRY(reset_sched(pool, 1, global, (uint32_t)grid, seed.target ? &seed : nullptr));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
@@ -825,8 +842,8 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // shard inside the seeding (UtsKind::seed_process) and then runs the
     // plain kernel; otherwise the worker loop itself filters (FEAT = 1)
     // (HX_UTS_SHARD_FILTER_IN_LOOP=1 builds the round-4 form for an A/B)
-    const bool seed_past_split = !HX_UTS_SHARD_FILTER_IN_LOOP && seed.target &&
-                                 split_depth < (int)seed.max_levels && split_depth + 1 < kSeedMaxLevels;
+    const bool seed_past_split = !HX_UTS_SHARD_FILTER_IN_LOOP && seed.target && nshards > 1 &&
+                                 seed.min_levels == (uint32_t)split_depth;
     const bool feat = max_levels > 0 || (nshards > 1 && (global || !seed_past_split));
     if (bin) ctx.bin_thr = (uint32_t)T.rules[1].y;
     const int mode = bin ? kUtsBin : geo_fixed ? kUtsGeoFixed : (ctx.lds_tables ? kUtsRulesLds : kUtsRulesGlobal);

@@ -1,7 +1,7 @@
 """Same-box A/B of T1XL's 8-shard partition (split 7, bench.py's N = 8
 wide-tree leg) between library builds: per build, every shard's kernel time
 and the whole tree's, best of `reps` (development aid).
-    python scripts/shard_ab.py reps name=lib.so ..."""
+    python scripts/shard_ab.py reps name=lib.so ...   (SPLIT=d: another split depth)"""
 import json
 import os
 import subprocess
@@ -14,13 +14,17 @@ import hclib_amd as H
 H.init(0)
 args = "-t 1 -a 3 -d 15 -b 4 -r 29"
 reps = int(sys.argv[2])
-shards = []
-for s in range(8):
+split = int(os.environ.get("SPLIT", "7"))
+shards = [None] * 8
+order = list(range(8))[::-1] if os.environ.get("ORDER") == "rev" else list(range(8))
+if os.environ.get("WARM", "1") == "1":
+    H.uts(args, order[-1], 8, split)  # the first launch of a process runs cold (shard_order.log)
+for s in order:
     best = None
     for _ in range(reps):
-        r = H.uts(args, s, 8, 7)
+        r = H.uts(args, s, 8, split)
         best = r["kernel_ms"] if best is None else min(best, r["kernel_ms"])
-    shards.append((r["nodes"], round(best, 3)))
+    shards[s] = (r["nodes"], round(best, 3))
 assert sum(n for n, _ in shards) == 1635119272
 whole = min(H.uts(args)["kernel_ms"] for _ in range(reps))
 print(json.dumps({"shards": shards, "whole": round(whole, 3), "feat": H.uts_last_launch()["feat"]}))
@@ -37,5 +41,6 @@ for a in sys.argv[2:]:
         continue
     d = json.loads(p.stdout.strip().splitlines()[-1])
     slow = max(t for _, t in d["shards"])
-    print(f"{name}: whole {d['whole']} ms, shards {[t for _, t in d['shards']]} ms, slowest {slow}, "
+    print(f"{name} split {os.environ.get('SPLIT', '7')} order {os.environ.get('ORDER', 'fwd')}: whole {d['whole']} ms, "
+          f"shards {[t for _, t in d['shards']]} ms, nodes (M) {[round(n / 1e6, 1) for n, _ in d['shards']]}, slowest {slow}, "
           f"projected efficiency {d['whole'] / (8 * slow):.3f}", flush=True)

@@ -42,6 +42,14 @@ t0 = tr[0, 1]
 ns = lambda x: float(x) * 10.0  # 100 MHz ticks -> ns
 hops = []
 t = ntw * nth - 1
+
+
+def since_start(t, k):
+    """stamp k of task t relative to its start, in ns; None when the build or
+    the task's path did not write it (a zero stamp)"""
+    return ns(tr[t, k] - tr[t, 1]) if tr[t, k] != 0 else None
+
+
 while t != 0:
     r = int(tr[t, 6])
     i, j = divmod(t, ntw)
@@ -49,15 +57,18 @@ while t != 0:
     kind = "row" if (ri, rj) == (i, j - 1) else "col" if (ri, rj) == (i - 1, j) else "diag"
     hops.append({"t": t, "kind": kind, "kept": int(tr[t, 4]),
                  "release": ns(tr[t, 0] - tr[r, 2]), "pickup": ns(tr[t, 1] - tr[t, 0]),
-                 "body": ns(tr[t, 2] - tr[t, 1]), "put": ns(tr[t, 3] - tr[t, 2]),
-                 # inside the body, from its start: ingress done, compute waves
-                 # 0 / 1 done, egress done (sw.hip SwDagWgKind stamps)
-                 "in_ingress": ns(tr[t, 8] - tr[t, 1]), "in_wave0": ns(tr[t, 10] - tr[t, 1]),
-                 "in_wave1": ns(tr[t, 11] - tr[t, 1]), "in_egress": ns(tr[t, 9] - tr[t, 1]),
-                 # waves 0 / 1: loop start (prologue done)
-                 "in_w0_loop": ns(tr[t, 12] - tr[t, 1]), "in_w1_loop": ns(tr[t, 15] - tr[t, 1]),
-                 # HCLIB_HIP_SW_PK=2 (sw_pk2_tile): wave B's inputs / first chunk (sweep end = in_w1_loop)
-                 "in_b_inputs": ns(tr[t, 13] - tr[t, 1]), "in_b_loop": ns(tr[t, 14] - tr[t, 1])})
+                 "body": ns(tr[t, 2] - tr[t, 1]),
+                 # the task's own put done (an early put, hx_dag.h kEarlyPut, lands
+                 # before the body's barrier: negative)
+                 "put": ns(tr[t, 3] - tr[t, 2]) if tr[t, 3] != 0 else None,
+                 # inside the body, from its start: inputs staged, first scores
+                 # there (loop start), sweep done, outputs issued
+                 "in_ingress": since_start(t, 8), "in_w0_loop": since_start(t, 12),
+                 "in_wave0": since_start(t, 10), "in_egress": since_start(t, 11),
+                 "in_entered": since_start(t, 14), "in_loaded": since_start(t, 15),
+                 # where the inputs came from (sw.hip trace word 13)
+                 "top_lds": int(tr[t, 13]) & 1, "top_mem": (int(tr[t, 13]) >> 1) & 1,
+                 "left_mem": (int(tr[t, 13]) >> 2) & 1, "corner_mem": (int(tr[t, 13]) >> 3) & 1})
     t = r
 hops.reverse()
 total = ns(tr[ntw * nth - 1, 2] - t0)
@@ -67,12 +78,21 @@ for kind in ("row", "col", "diag", "all"):
     hs = [h for h in hops if kind == "all" or h["kind"] == kind]
     if not hs:
         continue
-    res[kind] = {"hops": len(hs), "kept": sum(h["kept"] for h in hs)}
-    for k in ("release", "pickup", "body", "put", "in_ingress", "in_w0_loop", "in_wave0", "in_w1_loop", "in_wave1",
-              "in_egress", "in_b_inputs", "in_b_loop"):
-        v = np.array([h[k] for h in hs])
-        res[kind][k + "_us"] = round(float(v.mean()) / 1e3, 3)
-        res[kind][k + "_ms_total"] = round(float(v.sum()) / 1e6, 3)
+    res[kind] = {"hops": len(hs), "kept": sum(h["kept"] for h in hs),
+                 "top_from_lds": sum(h["top_lds"] for h in hs), "top_from_memory": sum(h["top_mem"] for h in hs),
+                 "left_from_memory": sum(h["left_mem"] for h in hs),
+                 "corner_from_memory": sum(h["corner_mem"] for h in hs)}
+    for k in ("release", "pickup", "body", "put", "in_entered", "in_loaded", "in_ingress", "in_w0_loop", "in_wave0",
+              "in_egress"):
+        v = [h[k] for h in hs if h[k] is not None]
+        res[kind][k + "_us"] = round(float(np.mean(v)) / 1e3, 3) if v else None
+        res[kind][k + "_ms_total"] = round(float(np.sum(v)) / 1e6, 3) if v else None
+    # per hop, the time that is not the sweep: release + pickup + body - sweep
+    sweep = [h["in_wave0"] - h["in_w0_loop"] for h in hs if h["in_wave0"] is not None and h["in_w0_loop"] is not None]
+    if sweep:
+        res[kind]["sweep_us"] = round(float(np.mean(sweep)) / 1e3, 3)
+        res[kind]["non_sweep_per_hop_us"] = round(
+            res[kind]["release_us"] + res[kind]["pickup_us"] + res[kind]["body_us"] - res[kind]["sweep_us"], 3)
 # every tile (not only the critical path): body and pickup distributions
 body = (tr[:, 2] - tr[:, 1]) * 10.0
 pick = (tr[1:, 1] - tr[1:, 0]) * 10.0
