@@ -747,18 +747,30 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // Rule-table trees (other shapes, HYBRID) of a few million nodes run
     // fastest with 4 (T2 1.80 -> 1.36 ms, T4 1.05 -> 0.86, T5 1.07 -> 0.96;
     // T2L still wants 8: profiles/r02/geo_spill.log)
+    // sharded launches of a rank attached to a global region share work
+    const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
+    // fixed-shape trees start seeded (breadth-first, hx_sched.h seed_levels)
+    const bool seed_on = geo_fixed && !global && env_int("HCLIB_HIP_UTS_SEED", 1);
     int wpc_default = 2, ring_default = 512;
     if (!bin) {
         const double est = uts_expected_nodes(*params);
-        // (fixed-shape trees start seeded, below: T1 then runs fastest on 4
-        // waves per CU and 512-item rings, 0.28 vs 0.61 ms unseeded on 2 / 256,
-        // profiles/r04/seed*_t1.log)
-        wpc_default = est >= 3e7 ? 8 : 4;
-        // and a small tree runs faster on 256-item rings (one piece per task:
-        // the frontier fans out by range splitting) at 2 waves per CU: T1
-        // 0.98 -> 0.70 ms; a large one slower (T1XL 52 -> 70 ms),
-        // profiles/r02/sweep_t1_ring_waves.log, sweep_t1xl_ring_waves.log, geo_lds_tail.log
-        ring_default = (est >= 3e7 || geo_fixed) ? 512 : 256;
+        if (seed_on) {
+            // seeded: every wave starts busy, so even a small tree fills 8
+            // waves per CU on 512-item rings once its seeding is cheap (round
+            // 5: T1 0.234 -> 0.220 ms at 8 waves per CU and 16 slots per wave,
+            // profiles/r05/sweep_t1_d.log; round 4 had 4 per CU, 0.28 vs 0.61
+            // ms unseeded on 2 / 256, profiles/r04/seed*_t1.log)
+            wpc_default = 8;
+            ring_default = 512;
+        } else {
+            wpc_default = est >= 3e7 ? 8 : (geo_fixed ? 2 : 4);
+            // an unseeded small tree runs faster on 256-item rings (one piece
+            // per task: the frontier fans out by range splitting), a fixed-shape
+            // one at 2 waves per CU: T1 0.98 -> 0.70 ms; a large one slower
+            // (T1XL 52 -> 70 ms), profiles/r02/sweep_t1_ring_waves.log,
+            // sweep_t1xl_ring_waves.log, geo_lds_tail.log
+            ring_default = est >= 3e7 ? 512 : 256;
+        }
     }
     const int grid = env_int("HCLIB_HIP_GRID", 0) > 0
                          ? env_int("HCLIB_HIP_GRID", 0)
@@ -774,8 +786,6 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // at one piece per task (T1XL 37.2 ms, T1L 3.77; profiles/r02/
     // pieces_tune.log; 336 at five pieces), 128 on 256-item rings (T1)
     const int ring_used = geo_fixed && !(nshards > 1 || max_levels > 0) ? env_int("HCLIB_HIP_UTS_RING", ring_default) : 512;
-    // sharded launches of a rank attached to a global region share work
-    const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
     // BIN trees: 66 since the register carry went through LDS (T3L 30.64 ->
     // 30.20 ms same-box against 72, profiles/r04/sc_ab_t3l*.log, t3l3_spill.log);
     // it must stay above one batch (64) or the narrow loop never runs
@@ -784,7 +794,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // keeps more before it feeds others: T1 0.285 -> 0.248 ms at 336, T1L
     // 2.70 -> 2.38, T1XL's 8-way shards 4.94 -> 4.75 at 448
     // (profiles/r04/seed5_*.log, seed6_*.log)
-    const bool seeded = geo_fixed && !global && env_int("HCLIB_HIP_UTS_SEED", 1) && ring_used >= 512;
+    const bool seeded = seed_on && ring_used >= 512;
     if (seeded) spill_lo_default = uts_expected_nodes(*params) >= 3e7 ? 448 : 336;
     cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_SPILL_LO", spill_lo_default);
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
@@ -811,7 +821,11 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         // slots per wave: a few for a small tree (one level fewer to expand),
         // more for a large one (finer shares, less stealing later;
         // profiles/r04/seed3_*.log, seed4_*.log)
-        const int per_wave = env_int("HCLIB_HIP_SEED_PER_WAVE", uts_expected_nodes(*params) >= 3e7 ? 32 : 4);
+        // (16 for small trees since round 5: one level deeper, T1 0.234 ->
+        // 0.220 ms, profiles/r05/sweep_t1_d.log; a level holds at most ~b x
+        // the target, so 32 keeps a wave's share of a b = 4 level within
+        // half its ring)
+        const int per_wave = env_int("HCLIB_HIP_SEED_PER_WAVE", uts_expected_nodes(*params) >= 3e7 ? 32 : 16);
         seed.target = (uint32_t)(grid * per_wave);
         seed.max_levels = (uint32_t)env_int("HCLIB_HIP_SEED_LEVELS", 20);
         // a shard's share is only known past its split (level d holds the

@@ -150,8 +150,8 @@ def test_uts_small_trees_bit_exact(golden, name):
 
 @pytest.mark.parametrize("name,want", [
     # bench.py's T1 launch: the plain kernel (no per-level counts), fixed-shape
-    # GEO, breadth-first seeded, 512-item rings, 4 waves per CU
-    ("T1", {"mode": "geo_fixed", "feat": 0, "seeded": 1, "ring": 512, "waves_per_cu": 4,
+    # GEO, breadth-first seeded, 512-item rings, 8 waves per CU
+    ("T1", {"mode": "geo_fixed", "feat": 0, "seeded": 1, "ring": 512, "waves_per_cu": 8,
             "workers_per_group": 1}),
     # BIN: two worker waves per workgroup (LDS inboxes), the plain kernel
     ("T3", {"mode": "bin", "feat": 0, "seeded": 0, "ring": 1024, "workers_per_group": 2}),
@@ -167,6 +167,18 @@ def test_uts_bench_launch_shape_bit_exact(golden, name, want):
     shape = H.uts_last_launch()
     for k, v in want.items():
         assert shape[k] == v, (name, k, shape)
+
+
+def test_uts_unseeded_fixed_shape(golden, monkeypatch):
+    """T1 with the seeding off (HCLIB_HIP_UTS_SEED=0) takes the unseeded
+    shape — 2 waves per CU on 256-item rings, as measured before seeding
+    existed (round-4 advisor) — and is bit-exact."""
+    monkeypatch.setenv("HCLIB_HIP_UTS_SEED", "0")
+    pub = golden("uts_goldens.json")["published"]["T1"]
+    r = H.uts(pub["args"])
+    assert (r["nodes"], r["leaves"], r["max_depth"]) == (pub["nodes"], pub["leaves"], pub["depth"])
+    shape = H.uts_last_launch()
+    assert (shape["seeded"], shape["ring"], shape["waves_per_cu"]) == (0, 256, 2), shape
 
 
 @pytest.mark.parametrize("name", ["T3L", "T1L"])
