@@ -539,12 +539,15 @@ __device__ __forceinline__ void kind_drain(const typename Kind::Ctx &ctx, typena
 // is low, the ticket is taken at once (one fetch-add, the head read beside
 // it refreshes `occ`); once it was high, the occupancy is read first and a
 // ring at least half full is refused, so a ticket never waits behind a
-// consumer that cannot come. With `pc`, the publish is deferred (see
-// PendingChunk); the caller must publish a live one before the next enqueue.
+// consumer that cannot come. With `defer`, the publish is deferred into `pc`
+// (see PendingChunk); the caller must publish a live one before the next
+// enqueue. (`pc` is a reference, never a pointer that may be null: a
+// select between a local's address and null keeps the local in scratch
+// memory, and every batch then read its `live` flag behind a vmcnt(0) wait.)
 template <class Kind, int CAP>
 __device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &pool, SchedGlobals *g, uint32_t q,
-                              WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n, uint32_t &occ, PendingChunk *pc,
-                              bool relief = false) {
+                              WaveStack<Kind, CAP> &st, uint32_t bot, uint32_t n, uint32_t &occ, PendingChunk &pc,
+                              bool defer, bool relief = false) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     QueueHdr *h = &pool.hdr[q];
@@ -604,11 +607,11 @@ __device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &poo
         }
     }
     if (lane == 0) st_agent(slot_ctl(pool, slot) + 1, n);
-    if (pc) {
-        pc->slot = slot;
-        pc->pos = pos;
-        pc->q = q;
-        pc->live = true;
+    if (defer) {
+        pc.slot = slot;
+        pc.pos = pos;
+        pc.q = q;
+        pc.live = true;
         return true;
     }
     handoff_publish();
@@ -1859,10 +1862,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 if (n > pool.chunk) n = pool.chunk;
                 bool ok = false;
                 for (uint32_t a = 0; a < pool.nq && !ok; ++a)
-                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr);
+                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, (home + a) % pool.nq, st, bot, n, occ, pend, false);
                 // every deque is at its half mark: fill one past it rather than wait
                 for (uint32_t a = 0; a < pool.nq && !ok; ++a)
-                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, (home + a) % pool.nq, st, bot, n, occ, nullptr, true);
+                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, (home + a) % pool.nq, st, bot, n, occ, pend, false,
+                                                  true);
                 if (!ok) {
                     // every deque is full: other waves are draining them, so wait
                     // (bounded) rather than fail at once
@@ -2085,7 +2089,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 // where the chunk goes: the home deque first, then the XCD's others
                 for (uint32_t a = 0; a < qpx && !ok; ++a) {
                     const uint32_t q = xcc * qpx + (home - xcc * qpx + a) % qpx;
-                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, q, st, bot, n, occ, cfg.defer ? &pend : nullptr);
+                    ok = enqueue_chunk<Kind, CAP>(ctx, pool, g, q, st, bot, n, occ, pend, cfg.defer != 0);
                 }
                 if (!ok) break;  // deques full: keep the items (the ring still has room)
                 ++npush;
