@@ -641,9 +641,20 @@ def main():
             cal = [(H.sha1_calibrate(ch, wpc, 2000)[0], ch, wpc) for ch, wpc in ((1, 12), (2, 12), (1, 16))]
             peak, ch, wpc = max(cal)
             ach = 1635119272 / (wide["kernel_ms_per_rank"][0] * 1e-3)
+            # the same ceiling priced from the per-instruction issue costs
+            # measured on this part (profiles/r04/ub_valu2.log, 4 waves per
+            # SIMD): the compiled SHA-1's mix (uts_sha1.h: 221 alignbit, 142
+            # add3 at 4.27 SIMD-cycles; 133 bitop3 at 2.64; 58 xor, 21 add at
+            # 2.42) = ~2,092 SIMD-cycles per wave-SHA-1 = 64 SHA-1 per SIMD
+            # per 2,092 cycles over every SIMD at the clock
+            simd_cycles = 221 * 4.27 + 142 * 4.27 + 133 * 2.64 + 58 * 2.42 + 21 * 2.42
+            issue_peak = 256 * 4 * 64 / simd_cycles * 2.4e9
             out["roofline_uts"] = {
                 "bound": "valu", "kernel": "k_uts_search (UTS T1XL, throughput-bound wide tree)",
                 "achieved": ach, "peak": peak, "unit": "nodes/s", "frac": ach / peak,
+                "peak_issue_model": issue_peak, "frac_issue_model": ach / issue_peak,
+                "issue_model": "uts_sha1.h's 575 VALU at the measured per-instruction issue costs "
+                               "(ub_valu2.log): %.0f SIMD-cycles per wave-SHA-1, 1,024 SIMDs, 2.4 GHz" % simd_cycles,
                 "peak_source": f"hclib_hip_sha1_calibrate: the rng_spawn SHA-1 of uts_sha1.h back to back, "
                                f"best of {[(round(c[0] / 1e9, 1), c[1], c[2]) for c in cal]} "
                                f"(G SHA-1/s, chains per lane, waves per CU)",
