@@ -119,6 +119,35 @@ __device__ __forceinline__ void acquire_agent() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ------------------------------------------------------------ LDS flags
+// Words that the waves of one workgroup hand to each other through LDS
+// (inbox states, counts). The LDS performs one wave's DS operations in issue
+// order, so a flag stored after the data it guards is seen after that data
+// by a wave that reads the flag first. These go through address-space-3
+// pointers: a `volatile` (or atomic) access through a generic pointer
+// compiles to a FLAT operation, which waits for the wave's global memory
+// traffic too (vmcnt) and leaves the DS queue, so it is not ordered with the
+// wave's ds_write of the data.
+typedef __attribute__((address_space(3))) uint32_t hx_lds_u32;
+__device__ __forceinline__ uint32_t lds_load(const uint32_t *p) {
+    asm volatile("" ::: "memory");
+    const uint32_t v = __hip_atomic_load((const hx_lds_u32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_store(uint32_t *p, uint32_t v) {
+    asm volatile("" ::: "memory");
+    __hip_atomic_store((hx_lds_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ bool lds_cas(uint32_t *p, uint32_t expected, uint32_t desired) {
+    asm volatile("" ::: "memory");
+    const bool ok = __hip_atomic_compare_exchange_strong((hx_lds_u32 *)p, &expected, desired, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    return ok;
+}
+
 // ------------------------------------------------------------ wave utils
 // hclib_get_current_worker / hclib_get_num_workers in device code
 // (src/hclib-runtime.c:194-226): a device worker is one wave of the launch,

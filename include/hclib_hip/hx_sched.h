@@ -1193,13 +1193,7 @@ __device__ bool inbox_put(const typename Kind::Ctx &ctx, Inbox<Kind> &ib, WaveSt
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     uint32_t ok = 0;
-    if (lane == 0) {
-        uint32_t expect = 0u;
-        ok = __hip_atomic_compare_exchange_strong(&ib.state, &expect, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP)
-                 ? 1u
-                 : 0u;
-    }
+    if (lane == 0) ok = lds_cas(&ib.state, 0u, 2u) ? 1u : 0u;
     if (!lane0(ok)) return false;
     {
         const bool valid = (uint32_t)lane < n;
@@ -1218,9 +1212,9 @@ __device__ bool inbox_put(const typename Kind::Ctx &ctx, Inbox<Kind> &ib, WaveSt
     asm volatile("" ::: "memory");
     if (lane == 0) {
         add_agent(&g->outstanding, 1u);  // the chunk's unit, before it becomes visible
-        *(volatile uint32_t *)&ib.n = n;
-        *(volatile uint32_t *)&ib.idle = 0u;
-        *(volatile uint32_t *)&ib.state = 1u;
+        lds_store(&ib.n, n);
+        lds_store(&ib.idle, 0u);
+        lds_store(&ib.state, 1u);  // after the items (one wave's DS operations land in order)
     }
     return true;
 }
@@ -1230,9 +1224,8 @@ template <class Kind, int CAP>
 __device__ uint32_t inbox_take(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
-    if (lane0(*(volatile uint32_t *)&ib.state) != 1u) return 0;
-    asm volatile("" ::: "memory");
-    const uint32_t n = lane0(*(volatile uint32_t *)&ib.n);
+    if (lane0(lds_load(&ib.state)) != 1u) return 0;
+    const uint32_t n = lane0(lds_load(&ib.n));
     if ((uint32_t)lane < n) {
         uint32_t w[W];
 #pragma unroll
@@ -1240,8 +1233,7 @@ __device__ uint32_t inbox_take(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st) {
         store_tmpl<Kind, CAP>(st, (uint32_t)lane, w);
         st.d[lane] = make_uint2(w[W - 2], w[W - 1]);
     }
-    asm volatile("" ::: "memory");
-    if (lane == 0) *(volatile uint32_t *)&ib.state = 0u;
+    if (lane == 0) lds_store(&ib.state, 0u);
     return n;
 }
 
@@ -1678,7 +1670,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 wave_goes_idle<GLOBAL>(g, gv, pool);
                 tl.log(kTlIdle, 0);
                 if constexpr (WPG > 1) {
-                    if (lane == 0) *(volatile uint32_t *)&ib[wave].idle = 1u;
+                    if (lane == 0) lds_store(&ib[wave].idle, 1u);
                 }
             }
             // probe order: home, a hint (the last deque pushed in an XCD's
@@ -1715,7 +1707,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 }
             }
             if constexpr (WPG > 1) {
-                if (n && lane == 0) *(volatile uint32_t *)&ib[wave].idle = 0u;
+                if (n && lane == 0) lds_store(&ib[wave].idle, 0u);
             }
             if constexpr (GLOBAL) {
                 // every 4th probe that found nothing local: the global ring
@@ -2080,8 +2072,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     // an idle sibling of this workgroup first (LDS, no HBM round trip)
                     for (uint32_t a = 1; a < (uint32_t)WPG && !ok; ++a) {
                         Inbox<Kind> &sib = ib[(wave + a) % (uint32_t)WPG];
-                        if (lane0(*(volatile uint32_t *)&sib.idle) == 1u &&
-                            lane0(*(volatile uint32_t *)&sib.state) == 0u)
+                        if (lane0(lds_load(&sib.idle)) == 1u && lane0(lds_load(&sib.state)) == 0u)
                             ok = inbox_put<Kind, CAP>(ctx, sib, st, bot, n, g);
                     }
                 }
@@ -2121,10 +2112,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     if constexpr (WPG > 1) {
         // close this wave's inbox: no sibling may hand it work any more
         if (lane == 0) {
-            *(volatile uint32_t *)&ib[wave].idle = 0u;
-            uint32_t expect = 0u;
-            __hip_atomic_compare_exchange_strong(&ib[wave].state, &expect, 3u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            lds_store(&ib[wave].idle, 0u);
+            (void)lds_cas(&ib[wave].state, 0u, 3u);
         }
     }
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
