@@ -289,9 +289,6 @@ struct SchedConfig {
 //        dependency chains fill each other's issue slots: a dependent chain of
 //        one wave issues a VALU op only every ~4-5 cycles of the 2 it needs)
 
-#ifndef HX_SPILL_GATE
-#define HX_SPILL_GATE 0
-#endif
 // Range items one task's children are pushed as (Kind::kPieces, default 8):
 // a task with c children becomes min(c, pieces) items. Fewer pieces need a
 // smaller ring (one batch pushes at most 64 * (pieces + 2) items), so a
@@ -2062,14 +2059,6 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         uint32_t sz = top - bot;
         uint32_t hungry = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
         const uint32_t lo = cfg.spill_lo;
-        // HX_SPILL_GATE (A/B): with fewer hungry waves than busy ones, each
-        // busy wave answers the (global) hunger signal only with probability
-        // hungry / busy, so the gifts add up to about the hunger instead of
-        // every busy wave giving at once
-        if (HX_SPILL_GATE && hungry > 0 && sz >= lo && sz <= cfg.spill_hi && hungry < outst) {
-            const uint32_t r = lane0(xorshift(rng));
-            if ((unsigned long long)r * outst >= ((unsigned long long)hungry << 32)) hungry = 0;
-        }
         if (sz > cfg.spill_hi || (hungry > 0 && sz >= lo)) {
             const unsigned long long ts = __builtin_amdgcn_s_memtime();
             const uint32_t cmax = pool.chunk;
