@@ -63,6 +63,7 @@ struct UtsCtx {
     const int4 *rules;
     const uint32_t *thr;
     unsigned long long *hist;
+    const uint32_t *chain;  // FEAT 3 (diagnostic): chain[d] = child index of the traced chain's depth-d node
 };
 
 constexpr size_t kUtsLdsRules = 64;     // depth rules cached in LDS per wave
@@ -166,7 +167,12 @@ constexpr int uts_pieces() {
 // 2: diagnostic trace (HCLIB_HIP_UTS_TRACE=1): per depth, the earliest
 // s_memrealtime (100 MHz) at which any wave reached it, recorded by a wave
 // only when its own deepest depth grows (the level_hist array receives
-// these times instead of counts)
+// these times instead of counts); 3: chain stamps (HCLIB_HIP_UTS_TRACE=2,
+// BIN trees): one given root-to-leaf chain (HCLIB_HIP_UTS_CHAIN, a file from
+// scripts/critpath/uts_chain.c) is followed through the search — its nodes
+// carry a flag in the height word's top bit — and level_hist[2d], [2d+1]
+// receive when its depth-d node ran and where (worker, narrow loop or not,
+// batch fill, dual batch)
 template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512)>
 struct UtsKind {
     // template = the node {state[5], height}; an item = its children [k, kend)
@@ -214,7 +220,7 @@ struct UtsKind {
             if (c.hist && c.hist_levels > 0) atomicAdd(&c.hist[0], 1ull);
         }
         for (int k = 0; k < 5; ++k) tmpl[k] = c.root[k];
-        tmpl[5] = 0;
+        tmpl[5] = FEAT == 3 ? 0x80000000u : 0u;  // FEAT 3: the root heads the traced chain
         return c.root_nc;
     }
 
@@ -223,7 +229,7 @@ struct UtsKind {
     template <int F = FEAT>
     __device__ static __forceinline__ int finish(const Ctx &c, Acc &acc, const uint32_t *t, const uint32_t *ch,
                                                  uint32_t *child, uint32_t *err, bool valid) {
-        const int h1 = (int)t[5] + 1;
+        const int h1 = (int)(F == 3 ? t[5] & 0x7fffffffu : t[5]) + 1;
         bool counted = valid;
         if (F && c.nshards > 1) {
             if (h1 == c.split && (ch[0] % (uint32_t)c.nshards) != (uint32_t)c.shard) return 0;
@@ -241,11 +247,12 @@ struct UtsKind {
             const uint32_t dm = wave_max(counted ? (uint32_t)h1 : 0u);
             if (dm > acc.trace_seen) {
                 acc.trace_seen = dm;
-                // stamp = time << 17 | worker (16 bits) << 1 | reached in the
-                // narrow loop (1) or not
+                // stamp = time (low 46 bits: 8 days of 100 MHz ticks, so a box up
+                // longer does not push every stamp past the 0xff.. fill) << 17 |
+                // worker (16 bits) << 1 | reached in the narrow loop (1) or not
                 if (lane_id() == 0 && (int)dm < c.hist_levels)
                     __hip_atomic_fetch_min(&c.hist[dm],
-                                           ((unsigned long long)__builtin_amdgcn_s_memrealtime() << 17) |
+                                           ((__builtin_amdgcn_s_memrealtime() & 0x3fffffffffffull) << 17) |
                                                ((unsigned long long)(acc.wid & 0xffffu) << 1) | acc.mode,
                                            __ATOMIC_RELAXED, HX_AGENT);
             }
@@ -260,12 +267,36 @@ struct UtsKind {
         return nc;
     }
 
+    // FEAT 3: the traced chain's next child index, loaded before the SHA-1
+    // by lanes whose node is on the chain (its latency hides behind it)
+    __device__ static __forceinline__ uint32_t chain_next(const Ctx &c, const uint32_t *t, bool valid) {
+        uint32_t kc = 0xffffffffu;
+        if (FEAT == 3 && valid && (t[5] >> 31)) kc = c.chain[(t[5] & 0x7fffffffu) + 1u];
+        return kc;
+    }
+    __device__ static __forceinline__ void chain_stamp(const Ctx &c, const Acc &acc, uint32_t *child, bool on,
+                                                       bool valid, uint32_t dual) {
+        if constexpr (FEAT == 3) {
+            const uint32_t fill = (uint32_t)__builtin_popcountll(__ballot(valid));
+            if (on) {
+                const uint32_t d = child[5];
+                child[5] = d | 0x80000000u;
+                c.hist[2 * d] = __builtin_amdgcn_s_memrealtime();
+                c.hist[2 * d + 1] = (unsigned long long)((acc.wid & 0xffffu) | (acc.mode << 16) | (dual << 17) |
+                                                         (fill << 20));
+            }
+        }
+    }
+
     __device__ static int process(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
                                   uint32_t *child, uint32_t *err, bool valid) {
         uint32_t ch[5];
+        const uint32_t kc = chain_next(c, t, valid);
         rng_spawn_dev(t, k, ch);
         for (int g = 1; g < c.gran; ++g) rng_spawn_dev(t, k, ch);  // -g: repeated spawns
-        return finish(c, acc, t, ch, child, err, valid);
+        const int nc = finish(c, acc, t, ch, child, err, valid);
+        chain_stamp(c, acc, child, k == kc, valid, 0u);
+        return nc;
     }
 
     // the breadth-first seeding's slots (hx_sched.h seed_levels) run with the
@@ -287,6 +318,7 @@ struct UtsKind {
                                     int &ncA, const uint32_t *tB, uint32_t kB, uint32_t *childB, int &ncB,
                                     uint32_t *err, bool validB) {
         uint32_t chA[5], chB[5];
+        const uint32_t kcA = chain_next(c, tA, true), kcB = chain_next(c, tB, validB);
         const uint32_t *pp[2] = {tA, tB};
         const uint32_t ii[2] = {kA, kB};
         uint32_t *oo[2] = {chA, chB};
@@ -294,6 +326,8 @@ struct UtsKind {
         for (int g = 1; g < c.gran; ++g) rng_spawn_n<2>(pp, ii, oo);  // -g: repeated spawns
         ncA = finish(c, acc, tA, chA, childA, err, true);
         ncB = finish(c, acc, tB, chB, childB, err, validB);
+        chain_stamp(c, acc, childA, kA == kcA, true, 1u);
+        chain_stamp(c, acc, childB, kB == kcB, validB, 1u);
     }
 };
 
@@ -697,8 +731,27 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     void *dmem = nullptr;
     if (max_levels) HX_HIP(hipMalloc(&dmem, hb));
     unsigned long long *d_hist = (unsigned long long *)dmem;
-    const bool trace = env_int("HCLIB_HIP_UTS_TRACE", 0) != 0 && max_levels > 0;
+    const int trace_kind = max_levels > 0 ? env_int("HCLIB_HIP_UTS_TRACE", 0) : 0;
+    const bool trace = trace_kind != 0;
     if (max_levels) HX_HIP(hipMemsetAsync(d_hist, trace ? 0xff : 0, hb, m.stream));
+    // FEAT 3 (diagnostic): the chain to follow, k_1..k_D of scripts/critpath/uts_chain.c
+    uint32_t *d_chain = nullptr;
+    if (trace_kind == 2) {
+        std::vector<uint32_t> chain;
+        const char *path = getenv("HCLIB_HIP_UTS_CHAIN");
+        if (FILE *f = path ? fopen(path, "rb") : nullptr) {
+            uint32_t w;
+            while (fread(&w, 4, 1, f) == 1) chain.push_back(w);
+            fclose(f);
+        }
+        if (chain.empty() || chain[0] + 1 != chain.size() || (size_t)max_levels < 2 * chain.size()) {
+            (void)hipFree(dmem);
+            set_error("hclib_hip_uts_search: chain trace needs HCLIB_HIP_UTS_CHAIN and max_levels >= 2 (D + 1)");
+            return HCLIB_HIP_EINVAL;
+        }
+        HX_HIP(hipMalloc(&d_chain, chain.size() * 4));
+        HX_HIP(hipMemcpy(d_chain, chain.data(), chain.size() * 4, hipMemcpyHostToDevice));
+    }
 
     UtsCtx ctx;
     memcpy(ctx.root, T.root, sizeof(ctx.root));
@@ -714,6 +767,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     ctx.rules = d_rules;
     ctx.thr = d_thr;
     ctx.hist = max_levels ? d_hist : nullptr;
+    ctx.chain = d_chain;
 
     ctx.lds_tables = (T.rules.size() <= kUtsLdsRules && T.thr.size() <= kUtsLdsThr) ? 1 : 0;
     ctx.bin_thr = 0;
@@ -872,10 +926,11 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     if (trace) {
         if (mode != kUtsBin || nshards > 1) {
             (void)hipFree(dmem);
+            if (d_chain) (void)hipFree(d_chain);
             set_error("hclib_hip_uts_search: the depth trace is for unsharded BIN trees");
             return HCLIB_HIP_EINVAL;
         }
-        kern = k_uts_search<kUtsBin, 2>;
+        kern = trace_kind == 2 ? k_uts_search<kUtsBin, 3> : k_uts_search<kUtsBin, 2>;
     }
     if (global) {
         static const uts_kernel_t gkernels[4] = {
@@ -892,11 +947,13 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // to each other through LDS before the HBM deques (T3L 34.0 -> 33.5-33.7
     // ms, profiles/r02/inbox_ab.log; HCLIB_HIP_WPG = 1, 2 or 4)
     int wpg = 1;
-    if (mode == kUtsBin && !global && !trace) {
+    if (mode == kUtsBin && !global && (!trace || trace_kind == 2)) {
         wpg = env_int("HCLIB_HIP_WPG", 2);
         if (wpg != 2 && wpg != 4) wpg = 1;
         if (grid % wpg) wpg = 1;
-        if (wpg == 2) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 2> : k_uts_search<kUtsBin, 0, 1024, false, 2>;
+        if (trace_kind == 2 && wpg == 4) wpg = 2;
+        if (trace_kind == 2 && wpg == 2) kern = k_uts_search<kUtsBin, 3, 1024, false, 2>;
+        else if (wpg == 2) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 2> : k_uts_search<kUtsBin, 0, 1024, false, 2>;
         if (wpg == 4) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 4> : k_uts_search<kUtsBin, 0, 1024, false, 4>;
     }
     {
@@ -905,7 +962,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
             const int ring = env_int("HCLIB_HIP_UTS_RING", ring_default);
             if (ring == 256 || ring == 1024) ring_k = ring;
         }
-        g_last_launch = hclib_hip_uts_launch_t{mode, trace ? 2 : (feat || global ? 1 : 0), wpg, grid, ring_k,
+        g_last_launch = hclib_hip_uts_launch_t{mode, trace ? 1 + trace_kind : (feat || global ? 1 : 0), wpg, grid, ring_k,
                                                seed.target ? 1 : 0, (int)seed.target, (int)cfg.spill_lo,
                                                grid / (m.num_cus > 0 ? m.num_cus : 1)};
     }
@@ -923,6 +980,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         for (int i = 0; i < max_levels; ++i) level_hist[i] = h[i];
     }
     (void)hipFree(dmem);
+    if (d_chain) (void)hipFree(d_chain);
     if (rc != HCLIB_HIP_OK) return rc;
     result->nodes = gl.counters[0];
     result->leaves = gl.counters[1];

@@ -33,7 +33,7 @@ raw = np.array(r["levels"], dtype=np.uint64)
 # (100 MHz time << 17) | worker << 1 | 1 when the batch that reached the
 # depth ran in the scheduler's narrow-frontier loop
 raw[0] = raw[1]
-ok = raw < np.uint64(2 ** 63)
+ok = raw != np.uint64(2 ** 64 - 1)  # unstamped depths keep the 0xff.. fill
 depth = int(ok.sum())
 narrow = (raw[:depth] & np.uint64(1)).astype(bool)
 wid = ((raw[:depth] >> np.uint64(1)) & np.uint64(0xffff)).astype(np.int64)
@@ -78,5 +78,13 @@ print(json.dumps({"edge_stays_on_worker": {"levels": int(same.sum()), "ns_per_le
                                                    "ns_per_level": round(float(step[~same].mean()), 1),
                                                    "ms": round(float(step[~same].sum()) / 1e6, 3)},
                   "distinct_workers_on_edge": int(len(set(wid[1:depth].tolist())))}), flush=True)
+# step-time distribution of the edge's same-worker steps, narrow loop or not
+for name, m in (("same_worker_narrow", same & nx), ("same_worker_main", same & ~nx)):
+    if m.any():
+        q = np.percentile(step[m] * ghz, [10, 50, 90, 99])
+        med = float(q[1])
+        print(json.dumps({name: {"levels": int(m.sum()), "cycles_p10_p50_p90_p99": [round(float(x)) for x in q],
+                                 "ms_above_1p5x_median": round(float(step[m][step[m] * ghz > 1.5 * med].sum()) / 1e6, 3),
+                                 "ms_at_median": round(med * int(m.sum()) / ghz / 1e6, 3)}}), flush=True)
 print(json.dumps({"summary": True, "excess_ms_total": round(tot_excess / ghz / 1e6, 3),
                   "worst_band": worst["depths"]}), flush=True)
