@@ -170,9 +170,10 @@ constexpr int uts_pieces() {
 // these times instead of counts); 3: chain stamps (HCLIB_HIP_UTS_TRACE=2,
 // BIN trees): one given root-to-leaf chain (HCLIB_HIP_UTS_CHAIN, a file from
 // scripts/critpath/uts_chain.c) is followed through the search — its nodes
-// carry a flag in the height word's top bit — and level_hist[2d], [2d+1]
+// carry a flag in the height word's top bit — and level_hist[4d], [4d+1]
 // receive when its depth-d node ran and where (worker, narrow loop or not,
-// batch fill, dual batch)
+// batch fill, dual batch), [4d+2], [4d+3] when it was given away and taken
+// if it changed hands (trace_item)
 template <int MODE, int FEAT, int CAP = (MODE == kUtsBin ? 1024 : 512)>
 struct UtsKind {
     // template = the node {state[5], height}; an item = its children [k, kend)
@@ -281,9 +282,24 @@ struct UtsKind {
             if (on) {
                 const uint32_t d = child[5];
                 child[5] = d | 0x80000000u;
-                c.hist[2 * d] = __builtin_amdgcn_s_memrealtime();
-                c.hist[2 * d + 1] = (unsigned long long)((acc.wid & 0xffffu) | (acc.mode << 16) | (dual << 17) |
+                c.hist[4 * d] = __builtin_amdgcn_s_memrealtime();
+                c.hist[4 * d + 1] = (unsigned long long)((acc.wid & 0xffffu) | (acc.mode << 16) | (dual << 17) |
                                                          (fill << 20));
+            }
+        }
+    }
+
+    // FEAT 3: an item {template, k, kend} holding the traced chain's next
+    // node changes hands (hx_sched.h kind_trace_item): level_hist[4d + 2] =
+    // when it was given away, [4d + 3] = when it was taken (bit 63: through
+    // a sibling's LDS inbox rather than the HBM deques)
+    __device__ static void trace_item(const Ctx &c, const uint32_t *w, bool valid, uint32_t ev, bool via_inbox) {
+        if constexpr (FEAT == 3) {
+            if (valid && (w[5] >> 31)) {
+                const uint32_t d = (w[5] & 0x7fffffffu) + 1u;
+                const uint32_t kc = c.chain[d];
+                if (kc >= w[kWords - 2] && kc < w[kWords - 1])
+                    c.hist[4 * d + ev] = __builtin_amdgcn_s_memrealtime() | (via_inbox ? 1ull << 63 : 0ull);
             }
         }
     }
@@ -685,7 +701,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
                                     int split_depth, hclib_hip_uts_result_t *result,
                                     uint64_t *level_hist, int max_levels) {
     if (!params || !result || nshards < 1 || shard < 0 || shard >= nshards || max_levels < 0 ||
-        max_levels > 65536 || (nshards > 1 && split_depth < 1)) {
+        max_levels > (env_int("HCLIB_HIP_UTS_TRACE", 0) == 2 ? 4 * 65536 : 65536) || (nshards > 1 && split_depth < 1)) {
         set_error("hclib_hip_uts_search: invalid arguments");
         return HCLIB_HIP_EINVAL;
     }
@@ -744,9 +760,9 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
             while (fread(&w, 4, 1, f) == 1) chain.push_back(w);
             fclose(f);
         }
-        if (chain.empty() || chain[0] + 1 != chain.size() || (size_t)max_levels < 2 * chain.size()) {
+        if (chain.empty() || chain[0] + 1 != chain.size() || (size_t)max_levels < 4 * chain.size()) {
             (void)hipFree(dmem);
-            set_error("hclib_hip_uts_search: chain trace needs HCLIB_HIP_UTS_CHAIN and max_levels >= 2 (D + 1)");
+            set_error("hclib_hip_uts_search: chain trace needs HCLIB_HIP_UTS_CHAIN and max_levels >= 4 (D + 1)");
             return HCLIB_HIP_EINVAL;
         }
         HX_HIP(hipMalloc(&d_chain, chain.size() * 4));

@@ -478,18 +478,32 @@ __device__ __forceinline__ uint32_t *slot_ctl(const PoolView &pool, uint32_t slo
 // producer publishes it after its next batch's body, when the payload stores
 // have long landed (the drain is free there) instead of waiting a round trip
 // for them while it holds the rest of its items.
+#ifndef HX_SPILL_X4
+#define HX_SPILL_X4 1  // chunk payloads as 16-byte sc1 stores / loads (enqueue_chunk, dequeue_chunk)
+#endif
 struct PendingChunk {
     uint32_t slot, pos, q;
     bool live;
 };
+
+// A compiler barrier behind a batch body's results: memory operations after
+// it (the deferred publish, its drain) stay after the body's arithmetic,
+// which has no memory operations of its own to order it
+template <int TW>
+__device__ __forceinline__ void after_body(const uint32_t *child) {
+#if HX_AFTER_BODY
+#pragma unroll
+    for (int i = 0; i < TW; ++i) asm volatile("" ::"v"(child[i]) : "memory");
+#endif
+}
 
 template <class Kind, int CAP>
 __device__ __forceinline__ void publish_pending(const PoolView &pool, SchedGlobals *g, PendingChunk &pc) {
     if (!pc.live) return;
     handoff_publish();  // the payload + cnt stores are complete
     if (lane_id() == 0) {
-        st_agent(slot_ctl(pool, pc.slot), pc.pos + 1);
-        st_agent(&g->hints[64u * ((pc.q / (pool.nq / 8u)) & 7u)], pc.q);
+        st_sc1_u32(slot_ctl(pool, pc.slot), pc.pos + 1);
+        st_sc1_u32(&g->hints[64u * ((pc.q / (pool.nq / 8u)) & 7u)], pc.q);
     }
     pc.live = false;
 }
@@ -507,6 +521,20 @@ struct kind_has_export<K, decltype((void)&K::export_item)> : std::true_type {};
 template <class Kind>
 __device__ __forceinline__ void kind_export(const typename Kind::Ctx &ctx, uint32_t *w, bool valid, uint32_t *err) {
     if constexpr (kind_has_export<Kind>::value) Kind::export_item(ctx, w, valid, err);
+}
+
+// Optional Kind hook (diagnostic traces): static void trace_item(const Ctx&,
+// const uint32_t *w, bool valid, uint32_t ev) — called by the whole wave for
+// items {template, k, kend} that change hands: ev 2 = given away (a chunk
+// or an inbox; `via_inbox`), 3 = taken by the receiving wave
+template <class K, class = void>
+struct kind_has_trace_item : std::false_type {};
+template <class K>
+struct kind_has_trace_item<K, decltype((void)&K::trace_item)> : std::true_type {};
+template <class Kind>
+__device__ __forceinline__ void kind_trace_item(const typename Kind::Ctx &ctx, const uint32_t *w, bool valid,
+                                                uint32_t ev, bool via_inbox) {
+    if constexpr (kind_has_trace_item<Kind>::value) Kind::trace_item(ctx, w, valid, ev, via_inbox);
 }
 
 // Optional Kind hooks: static bool seeding(const Ctx&) and
@@ -601,12 +629,24 @@ __device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &poo
         w[W - 2] = dd.x;
         w[W - 1] = dd.y & (kMaxChildren - 1);
         kind_export<Kind>(ctx, w, valid, &g->err);
+        kind_trace_item<Kind>(ctx, w, valid, 2u, false);
         if (valid) {
+            if constexpr (HX_SPILL_X4 && W % 4 == 0) {
+                // 16-byte sc1 stores (a dword sc1 store costs ~6x the bytes of
+                // a dwordx4 one), written as inline asm, which the compiler's
+                // waitcnt pass does not see: it would otherwise wait for them
+                // (vmcnt(0), and so for every load issued since) before the
+                // next batch reuses their data registers
 #pragma unroll
-            for (int i = 0; i < W; ++i) st_agent(&dst[(uint32_t)lane * W + i], w[i]);
+                for (int i = 0; i < W; i += 4)
+                    st_sc1_x4(&dst[(uint32_t)lane * W + i], make_uint4(w[i], w[i + 1], w[i + 2], w[i + 3]));
+            } else {
+#pragma unroll
+                for (int i = 0; i < W; ++i) st_agent(&dst[(uint32_t)lane * W + i], w[i]);
+            }
         }
     }
-    if (lane == 0) st_agent(slot_ctl(pool, slot) + 1, n);
+    if (lane == 0) st_sc1_u32(slot_ctl(pool, slot) + 1, n);
     if (defer) {
         pc.slot = slot;
         pc.pos = pos;
@@ -616,8 +656,8 @@ __device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &poo
     }
     handoff_publish();
     if (lane == 0) {
-        st_agent(slot_ctl(pool, slot), pos + 1);
-        st_agent(&g->hints[64u * ((q / (pool.nq / 8u)) & 7u)], q);
+        st_sc1_u32(slot_ctl(pool, slot), pos + 1);
+        st_sc1_u32(&g->hints[64u * ((q / (pool.nq / 8u)) & 7u)], q);
     }
     // nothing stays in flight past a spill (see vm_drain)
     vm_drain();
@@ -635,7 +675,7 @@ struct ProbeStats {
 };
 
 template <class Kind, int CAP>
-__device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Kind, CAP> &st,
+__device__ uint32_t dequeue_chunk(const typename Kind::Ctx &ctx, const PoolView &pool, uint32_t q, WaveStack<Kind, CAP> &st,
                                   SchedGlobals *g, uint32_t &done, ProbeStats &ps) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
@@ -690,14 +730,21 @@ __device__ uint32_t dequeue_chunk(const PoolView &pool, uint32_t q, WaveStack<Ki
     const uint32_t *src = pool.data + (size_t)slot * pool.chunk * W;
     if ((uint32_t)lane < n) {
         uint32_t w[W];
+        if constexpr (HX_SPILL_X4 && W == 8) {
+            uint4 a, b;
+            ld_sc1_x4x2(&src[(uint32_t)lane * W], a, b);
+            w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y, w[6] = b.z, w[7] = b.w;
+        } else {
 #pragma unroll
-        for (int i = 0; i < W; ++i) w[i] = ld_agent(&src[(uint32_t)lane * W + i]);
+            for (int i = 0; i < W; ++i) w[i] = ld_agent(&src[(uint32_t)lane * W + i]);
+        }
         store_tmpl<Kind, CAP>(st, (uint32_t)lane, w);
         st.d[lane] = make_uint2(w[W - 2], w[W - 1]);
+        kind_trace_item<Kind>(ctx, w, true, 3u, false);
     }
     // all reads of the slot have landed before it is handed back
     vm_drain();
-    if (lane == 0) st_agent(slot_ctl(pool, slot), pos + pool.cap);
+    if (lane == 0) st_sc1_u32(slot_ctl(pool, slot), pos + pool.cap);
     // one wave per workgroup: its LDS ops complete in issue order
     return n;
 }
@@ -1037,6 +1084,15 @@ struct NarrowState {
     uint32_t ck, carry, top, tag, n_exec, n_spawn, batches;
 };
 
+#ifndef HX_AFTER_BODY
+#define HX_AFTER_BODY 1
+#endif
+#ifndef HX_DRAIN_BEFORE_LOOP
+#define HX_DRAIN_BEFORE_LOOP 1
+#endif
+#ifndef HX_INBOX_NAP
+#define HX_INBOX_NAP 1  // idle siblings watch their inbox while backing off (run_worker)
+#endif
 #ifndef HX_NARROW_NOINLINE
 #define HX_NARROW_NOINLINE 0  // measured: inlined 34.1-34.5 ms vs 35.7-36.3 ms on T3L (profiles/r02/narrow_inline_ab.log)
 #endif
@@ -1204,6 +1260,7 @@ __device__ bool inbox_put(const typename Kind::Ctx &ctx, Inbox<Kind> &ib, WaveSt
         w[W - 2] = dd.x;
         w[W - 1] = dd.y & (kMaxChildren - 1);
         kind_export<Kind>(ctx, w, valid, &g->err);
+        kind_trace_item<Kind>(ctx, w, valid, 2u, true);
         if (valid) {
 #pragma unroll
             for (int i = 0; i < W; ++i) ib.w[(uint32_t)lane * W + i] = w[i];
@@ -1221,7 +1278,7 @@ __device__ bool inbox_put(const typename Kind::Ctx &ctx, Inbox<Kind> &ib, WaveSt
 
 // take a full inbox into the (empty) ring; returns the items (0: empty)
 template <class Kind, int CAP>
-__device__ uint32_t inbox_take(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st) {
+__device__ uint32_t inbox_take(const typename Kind::Ctx &ctx, Inbox<Kind> &ib, WaveStack<Kind, CAP> &st) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     if (lane0(lds_load(&ib.state)) != 1u) return 0;
@@ -1232,6 +1289,7 @@ __device__ uint32_t inbox_take(Inbox<Kind> &ib, WaveStack<Kind, CAP> &st) {
         for (int i = 0; i < W; ++i) w[i] = ib.w[(uint32_t)lane * W + i];
         store_tmpl<Kind, CAP>(st, (uint32_t)lane, w);
         st.d[lane] = make_uint2(w[W - 2], w[W - 1]);
+        kind_trace_item<Kind>(ctx, w, true, 3u, true);
     }
     if (lane == 0) lds_store(&ib.state, 0u);
     return n;
@@ -1648,6 +1706,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     bool busy_phase = true;
     uint32_t outst_pf = 0;  // lane 0: `outstanding` as loaded one batch ago
     uint32_t outst_cur = 0, hunger_in = 0;
+    // nothing from the set-up stays in flight into the loop: a load whose
+    // register the loop's first batch body overwrites would make the
+    // compiler wait (vmcnt(0)) there in every batch, and so for the
+    // one-batch-late hunger read
+    if (HX_DRAIN_BEFORE_LOOP) vm_drain();
     while (true) {
         // the ring bounds are wave-uniform: pin them to SGPRs (the uniformity
         // analysis cannot see through the loop's exits) so the batch's
@@ -1673,30 +1736,28 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                     if (lane == 0) lds_store(&ib[wave].idle, 1u);
                 }
             }
-            // probe order: home, a hint (the last deque pushed in an XCD's
+            // a sibling's inbox first (LDS, no round trip), then the deques.
+            // Probe order: home, a hint (the last deque pushed in an XCD's
             // slice: this wave's own XCD first, then the others in turn), then
             // random (3/4 same XCD, 1/4 anywhere)
-            uint32_t q = home;
-            const uint32_t phase = spins % 3;
-            if (phase == 1) {
-                uint32_t hq = 0;
-                if (lane == 0) hq = ld_agent(&g->hints[64u * ((xcc + spins / 3u) & 7u)]);
-                q = lane0(hq) % pool.nq;
-            } else if (phase == 2) {
-                uint32_t r = lane0(xorshift(rng));
-                q = ((r & 3) != 0) ? xcc * qpx + (r >> 2) % qpx : (r >> 2) % pool.nq;
-            }
             uint32_t n = 0, src = 0;
+            uint32_t q = home;
             if constexpr (WPG > 1) {
-                n = inbox_take<Kind, CAP>(ib[wave], st);  // inherits the chunk's unit
-                if (n) {
-                    q = home;
-                    src = 3;
-                }
+                n = inbox_take<Kind, CAP>(ctx, ib[wave], st);  // inherits the chunk's unit
+                if (n) src = 3;
             }
             uint32_t fin = 0;
             if (n == 0) {
-                n = dequeue_chunk<Kind, CAP>(pool, q, st, g, fin, pstat);
+                const uint32_t phase = spins % 3;
+                if (phase == 1) {
+                    uint32_t hq = 0;
+                    if (lane == 0) hq = ld_agent(&g->hints[64u * ((xcc + spins / 3u) & 7u)]);
+                    q = lane0(hq) % pool.nq;
+                } else if (phase == 2) {
+                    uint32_t r = lane0(xorshift(rng));
+                    q = ((r & 3) != 0) ? xcc * qpx + (r >> 2) % qpx : (r >> 2) % pool.nq;
+                }
+                n = dequeue_chunk<Kind, CAP>(ctx, pool, q, st, g, fin, pstat);
                 src = q == home ? 1 : 2;
             }
             if constexpr (!GLOBAL) {
@@ -1813,10 +1874,21 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 break;
             }
             // back off so idle pollers do not saturate the deque heads
-            // (cfg.backoff: the longest sleep, 16 = 1024 clocks)
-            if (spins < 8 || cfg.backoff <= 1) __builtin_amdgcn_s_sleep(1);
-            else if (spins < 64 || cfg.backoff <= 4) __builtin_amdgcn_s_sleep(4);
-            else __builtin_amdgcn_s_sleep(16);
+            // (cfg.backoff: the longest sleep, 16 = 1024 clocks). With
+            // siblings the sleep is cut into 64-clock naps that watch this
+            // wave's inbox (an LDS read): a sibling's hand-off is taken within
+            // one nap instead of after the sleep and the next deque probe
+            if constexpr (WPG > 1 && HX_INBOX_NAP) {
+                const uint32_t naps = (spins < 8 || cfg.backoff <= 1) ? 1u : (spins < 64 || cfg.backoff <= 4) ? 3u : 8u;
+                for (uint32_t i = 0; i < naps; ++i) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (lane0(lds_load(&ib[wave].state)) == 1u) break;
+                }
+            } else {
+                if (spins < 8 || cfg.backoff <= 1) __builtin_amdgcn_s_sleep(1);
+                else if (spins < 64 || cfg.backoff <= 4) __builtin_amdgcn_s_sleep(4);
+                else __builtin_amdgcn_s_sleep(16);
+            }
             continue;
         }
         ++nbatch;
@@ -1898,6 +1970,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 load_tmpl<Kind, CAP>(st, (pB - (dB.y >> 24)) & M, tB);
                 int ncA = 0, ncB = 0;
                 Kind::process2(ctx, acc, tA, kA, cA, ncA, tB, kB, cB, ncB, &g->err, hasB);
+                after_body<TW>(cA);
+                after_body<TW>(cB);
                 publish_pending<Kind, CAP>(pool, g, pend);
                 top -= take2;
                 const uint32_t rA = kendA - kA - 1u, rB = hasB ? kendB - kB - 1u : 0u;
@@ -1959,7 +2033,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             if (has) cnt = Kind::process(ctx, acc, tmpl, k, child, &g->err, true);
         }
         // the previous batch's spilled chunk: its payload stores landed while
-        // this batch ran
+        // this batch ran (after_body: the body's register-only work would
+        // otherwise be scheduled after the publish, whose drain then waited
+        // for those stores' whole round trip before the body)
+        after_body<TW>(child);
         publish_pending<Kind, CAP>(pool, g, pend);
         if (HX_STAMPS && cfg.stamps) {
             const unsigned long long ts1 = __builtin_amdgcn_s_memtime();

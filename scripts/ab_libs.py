@@ -21,6 +21,7 @@ for w in sys.argv[3:]:
     for _ in range(3):
         if w in TREES:
             r = H.uts(TREES[w][0]); assert r["nodes"] == TREES[w][1], (w, r["nodes"]); ms = r["kernel_ms"]
+            c = H.last_sched_counters(); out[w + "_mhz"] = round(100.0 * c[5] / max(1, c[6]))
         elif w.startswith("sw_"):
             s1 = H.sw_map(open(os.path.join(sys.argv[1], "tests/golden/sw/string1-huge.txt"), "rb").read())[:65536]
             s2 = H.sw_map(open(os.path.join(sys.argv[1], "tests/golden/sw/string2-huge.txt"), "rb").read())[:65536]
@@ -38,7 +39,7 @@ if "--" in args:
     i = args.index("--")
     args, work = args[:i], args[i + 1:]
 libs = [a.split("=", 1) for a in args]
-for rep in range(2):
+for rep in range(int(os.environ.get("REPS", "2"))):
     for name, path in libs:
         env = dict(os.environ, HCLIB_AMD_LIB=os.path.abspath(path))
         r = subprocess.run([sys.executable, "-c", CHILD, ROOT, json.dumps(TREES)] + work, env=env,

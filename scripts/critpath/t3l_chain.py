@@ -30,6 +30,8 @@ ALL = np.uint64(2 ** 64 - 1)
 def analyse(r, raw):
     t = raw[1:D + 1, 0]
     info = raw[1:D + 1, 1]
+    give_raw = raw[1:D + 1, 2]
+    take_raw = raw[1:D + 1, 3]
     if (t == ALL).any():
         return {"error": "unstamped depths", "missing": int((t == ALL).sum()),
                 "first_missing": int(np.argmax(t == ALL)) + 1}
@@ -57,6 +59,24 @@ def analyse(r, raw):
                      "cycles_p10_p50_p90_p99": [round(float(x)) for x in q],
                      "mean_fill": round(float(fill[1:][m].mean()), 1)}
     med = float(np.median(step[cats["same_narrow"]])) if cats["same_narrow"].any() else float(np.median(step))
+    # a move's parts: creation (the parent ran) -> given away -> taken -> run
+    top = np.uint64(1 << 63)
+    for name in ("moved_sibling", "moved_far"):
+        m = cats[name]
+        g = give_raw[1:][m]
+        k = take_raw[1:][m]
+        ok = (g != ALL) & (k != ALL)
+        if not ok.any():
+            continue
+        tg = (g[ok] & ~top).astype(np.float64) * 10.0
+        tk = (k[ok] & ~top).astype(np.float64) * 10.0
+        tc = t[:-1][m][ok]
+        tr = t[1:][m][ok]
+        parts = {"in_giver_ring": tg - tc, "handoff": tk - tg, "taker_to_run": tr - tk}
+        out[name]["parts_cycles_p50"] = {p: round(float(np.median(v)) * 2.4) for p, v in parts.items()}
+        out[name]["parts_ms"] = {p: round(float(v.sum()) / 1e6, 3) for p, v in parts.items()}
+        out[name]["stamped"] = int(ok.sum())
+        out[name]["via_inbox"] = int(((g[ok] & top) != 0).sum())
     out["ms_if_every_step_at_narrow_median"] = round(med * (D - 1) / 1e6, 3)
     out["excess_ms_by_category"] = {name: round(float((step[m] - med).sum()) / 1e6, 3) for name, m in cats.items()}
     return out
@@ -71,8 +91,8 @@ for cfg in configs:
     os.environ["HCLIB_HIP_UTS_TRACE"] = "2"
     os.environ["HCLIB_HIP_UTS_CHAIN"] = os.path.abspath(path)
     for ri in range(int(os.environ.get("RUNS", "1"))):
-        r = H.uts(T3L, max_levels=2 * (D + 1))
-        raw = np.array(r["levels"], dtype=np.uint64).reshape(-1, 2)
+        r = H.uts(T3L, max_levels=4 * (D + 1))
+        raw = np.array(r["levels"], dtype=np.uint64).reshape(-1, 4)
         out = {"config": cfg, "plain_ms": [round(x, 3) for x in plain], "run": ri,
                "nodes_ok": r["nodes"] == 111345631, "launch": H.uts_last_launch()}
         out.update(analyse(r, raw))
