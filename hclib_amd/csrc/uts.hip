@@ -821,7 +821,13 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
     // fixed-shape trees start seeded (breadth-first, hx_sched.h seed_levels)
     const bool seed_on = geo_fixed && !global && env_int("HCLIB_HIP_UTS_SEED", 1);
-    int wpc_default = 2, ring_default = 512;
+    // BIN trees: four worker waves per CU in one workgroup (one per SIMD;
+    // three siblings to hand work to through LDS before the HBM deques):
+    // T3L 29.08 -> 28.76 ms mean of 6 interleaved rounds against two per CU
+    // in pairs, T3 2.78 -> 2.76 (profiles/r05/sweep_wpg_t3l.log,
+    // sweep_wpg_t3.log; the critical chain's HBM hand-offs 560 -> 295,
+    // t3l_chain_wpg.jsonl). Launches that share work across ranks keep 2
+    int wpc_default = bin && !global ? 4 : 2, ring_default = 512;
     if (!bin) {
         const double est = uts_expected_nodes(*params);
         if (seed_on) {
@@ -959,18 +965,19 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         if (ring == 256) kern = k_uts_search<kUtsGeoFixed, 0, 256>;
         else if (ring == 1024) kern = k_uts_search<kUtsGeoFixed, 0, 1024>;
     }
-    // BIN trees: the two worker waves of a CU share a workgroup and hand work
-    // to each other through LDS before the HBM deques (T3L 34.0 -> 33.5-33.7
-    // ms, profiles/r02/inbox_ab.log; HCLIB_HIP_WPG = 1, 2 or 4)
+    // BIN trees: the worker waves of a CU share a workgroup and hand work
+    // to each other through LDS before the HBM deques (two: T3L 34.0 ->
+    // 33.5-33.7 ms, profiles/r02/inbox_ab.log; four since round 5, see
+    // wpc_default; HCLIB_HIP_WPG = 1, 2 or 4)
     int wpg = 1;
     if (mode == kUtsBin && !global && (!trace || trace_kind == 2)) {
-        wpg = env_int("HCLIB_HIP_WPG", 2);
+        wpg = env_int("HCLIB_HIP_WPG", 4);
         if (wpg != 2 && wpg != 4) wpg = 1;
         if (grid % wpg) wpg = 1;
-        if (trace_kind == 2 && wpg == 4) wpg = 2;
         if (trace_kind == 2 && wpg == 2) kern = k_uts_search<kUtsBin, 3, 1024, false, 2>;
+        else if (trace_kind == 2 && wpg == 4) kern = k_uts_search<kUtsBin, 3, 1024, false, 4>;
         else if (wpg == 2) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 2> : k_uts_search<kUtsBin, 0, 1024, false, 2>;
-        if (wpg == 4) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 4> : k_uts_search<kUtsBin, 0, 1024, false, 4>;
+        else if (wpg == 4) kern = feat ? k_uts_search<kUtsBin, 1, 1024, false, 4> : k_uts_search<kUtsBin, 0, 1024, false, 4>;
     }
     {
         int ring_k = mode == kUtsBin ? 1024 : 512;

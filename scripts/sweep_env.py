@@ -13,7 +13,8 @@ import torch
 import hclib_amd as H
 H.init(0)
 T = {"T1": ("-t 1 -a 3 -d 10 -b 4 -r 19", 4130071), "T3L": ("-t 0 -b 2000 -q 0.200014 -m 5 -r 7", 111345631),
-     "T1XL": ("-t 1 -a 3 -d 15 -b 4 -r 29", 1635119272), "T1L": ("-t 1 -a 3 -d 13 -b 4 -r 29", 102181082)}
+     "T1XL": ("-t 1 -a 3 -d 15 -b 4 -r 29", 1635119272), "T1L": ("-t 1 -a 3 -d 13 -b 4 -r 29", 102181082),
+     "T3": ("-t 0 -b 2000 -q 0.124875 -m 8 -r 42", 4112897)}
 args, nodes = T[os.environ["HX_TREE"]]
 ms = []
 for _ in range(3):

@@ -154,7 +154,7 @@ def test_uts_small_trees_bit_exact(golden, name):
     ("T1", {"mode": "geo_fixed", "feat": 0, "seeded": 1, "ring": 512, "waves_per_cu": 8,
             "workers_per_group": 1}),
     # BIN: two worker waves per workgroup (LDS inboxes), the plain kernel
-    ("T3", {"mode": "bin", "feat": 0, "seeded": 0, "ring": 1024, "workers_per_group": 2}),
+    ("T3", {"mode": "bin", "feat": 0, "seeded": 0, "ring": 1024, "workers_per_group": 4, "waves_per_cu": 4}),
 ])
 def test_uts_bench_launch_shape_bit_exact(golden, name, want):
     """The exact launch the bench runs (no max_levels: FEAT = 0, the kernel
