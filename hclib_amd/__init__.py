@@ -89,6 +89,7 @@ EXPORTS_HIP = [
     "hclib_hip_num_workers", "hclib_hip_uts_search", "hclib_hip_uts_num_children_host",
     "hclib_hip_uts_bucket_check", "hclib_hip_sha1_calibrate",
     "hclib_hip_fib", "hclib_hip_sw", "hclib_hip_last_sched_counters", "hclib_hip_last_narrow_counters",
+    "hclib_hip_last_phase_counters",
     "hclib_hip_sw_band_begin", "hclib_hip_sw_band_rows", "hclib_hip_sw_band_end",
 ]
 
@@ -378,6 +379,14 @@ def sha1_calibrate(chains: int = 1, waves_per_cu: int = 8, iters: int = 2000):
     _check(lib().hclib_hip_sha1_calibrate(chains, waves_per_cu, iters, C.byref(r), C.byref(ms)),
            "hclib_hip_sha1_calibrate")
     return r.value, ms.value
+
+
+def last_phase_counters():
+    """HX_PHASES builds: main-loop batch phase cycles of the last launch
+    (hclib_hip_last_phase_counters)."""
+    out = (C.c_uint64 * 8)()
+    lib().hclib_hip_last_phase_counters(out)
+    return list(out)
 
 
 def last_sched_counters():

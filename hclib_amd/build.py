@@ -45,7 +45,7 @@ VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "trace": ["-DHX_TRACE=1"], "timeline": 
             "sched_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
             # GEO 512-ring piece counts (uts.hip uts_pieces): fixed-shape trees at 5, rule tables at 1
             "fixed_pieces5": ["-DHX_UTS_FIXED_PIECES_512=5"], "rules_pieces1": ["-DHX_UTS_PIECES_512=1"],
-            "residual_whole": ["-DHX_RESIDUAL_WHOLE=1"], "seedfence1": ["-DHX_SEED_FENCES=1"], "shardloop": ["-DHX_UTS_SHARD_FILTER_IN_LOOP=1"], "nonap": ["-DHX_INBOX_NAP=0"], "spill1": ["-DHX_SPILL_X4=0"], "noafter": ["-DHX_AFTER_BODY=0"], "noasmst": ["-DHX_ASM_HANDOFF_STORES=0"], "nodrain": ["-DHX_DRAIN_BEFORE_LOOP=0"],
+            "residual_whole": ["-DHX_RESIDUAL_WHOLE=1"], "seedfence1": ["-DHX_SEED_FENCES=1"], "shardloop": ["-DHX_UTS_SHARD_FILTER_IN_LOOP=1"], "nonap": ["-DHX_INBOX_NAP=0"], "spill1": ["-DHX_SPILL_X4=0"], "noafter": ["-DHX_AFTER_BODY=0"], "noasmst": ["-DHX_ASM_HANDOFF_STORES=0"], "nodrain": ["-DHX_DRAIN_BEFORE_LOOP=0"], "phases": ["-DHX_PHASES=1"],
             "split3": ["-DHX_RESIDUAL_SPLIT_MIN=3"], "split4": ["-DHX_RESIDUAL_SPLIT_MIN=4"],
             "split8": ["-DHX_RESIDUAL_SPLIT_MIN=8"]}
 

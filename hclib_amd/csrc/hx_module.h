@@ -27,6 +27,7 @@ struct Module {
     SchedGlobals *globals = nullptr;
     unsigned long long last_counters[16] = {};  // counters of the last megakernel launch
     unsigned long long last_narrow[4] = {};     // SchedGlobals::narrow of the last launch
+    unsigned long long last_phase[8] = {};      // HX_PHASES builds (hclib_hip_last_phase_counters)
     // per-wave records of megakernel launches (WaveStat, hx_sched.h)
     WaveStat *wave_stats = nullptr;
     uint32_t wave_stats_cap = 0;

@@ -231,6 +231,7 @@ int finish_sched(SchedGlobals *host_copy, const char *who) {
     // the workers' exit records (every worker of the grid writes its own)
     static std::vector<unsigned long long> rec;
     const uint32_t nrec = m.rec_workers;
+    for (int i = 0; i < 8; ++i) m.last_phase[i] = 0;
     m.rec_workers = 0;
     if (nrec) {
         rec.resize((size_t)nrec * kWaveCtrWords);
@@ -245,6 +246,8 @@ int finish_sched(SchedGlobals *host_copy, const char *who) {
         for (int i = 0; i < 4; ++i)
             if (r[16 + i] > host_copy->maxes[i]) host_copy->maxes[i] = r[16 + i];
         for (int i = 0; i < 3; ++i) host_copy->narrow[i] += r[20 + i];
+        m.last_phase[0] += r[23];
+        for (int i = 0; i < 4; ++i) m.last_phase[1 + i] += r[28 + i];
     }
     memcpy(m.last_counters, host_copy->counters, sizeof(m.last_counters));
     memcpy(m.last_narrow, host_copy->narrow, sizeof(m.last_narrow));
@@ -336,6 +339,12 @@ void *hclib_hip_stream(void) { return g_mod.inited ? (void *)g_mod.stream : null
 
 void hclib_hip_last_sched_counters(uint64_t out[16]) {
     for (int i = 0; i < 16; ++i) out[i] = g_mod.last_counters[i];
+}
+
+// HX_PHASES builds: [0] main-loop single batches, [1..4] s_memtime cycles
+// summed over them: loop top -> pop issued -> pop landed -> body -> batch end
+extern "C" void hclib_hip_last_phase_counters(uint64_t out[8]) {
+    for (int i = 0; i < 8; ++i) out[i] = g_mod.last_phase[i];
 }
 
 void hclib_hip_last_narrow_counters(uint64_t out[4]) {

@@ -888,6 +888,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // whose ring fits two batches' pushes: the fixed-shape GEO trees on
     // 512-item rings)
     cfg.dual = (uint32_t)env_int("HCLIB_HIP_UTS_DUAL", 1);
+    cfg.spills = (uint32_t)env_int("HCLIB_HIP_SPILLS_PER_BATCH", 0);
     // breadth-first seeding (hx_sched.h seed_levels) for fixed-shape GEO
     // trees: the grid expands the top levels together and shares the level
     // that reaches HCLIB_HIP_SEED_PER_WAVE slots per wave out evenly, instead

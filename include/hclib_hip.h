@@ -94,6 +94,10 @@ int hclib_hip_last_wave_stats(hclib_hip_wave_stats_t *out, int max);
 /* The narrow-frontier carry loop of the last launch (hx_sched.h): [0]
  * batches run in it, [1] shader-clock cycles spent in it, [2] entries. */
 void hclib_hip_last_narrow_counters(uint64_t out[4]);
+/* Diagnostic (HX_PHASES builds, zeros otherwise): [0] main-loop single
+ * batches of the last megakernel launch, [1..4] their s_memtime cycles from
+ * loop top to pop issued, pop landed, body done, batch end. */
+void hclib_hip_last_phase_counters(uint64_t out[8]);
 /* Worker timelines of the last megakernel launch (diagnostic: a library
  * built with `--variant timeline` and HCLIB_HIP_TIMELINE=<events per
  * worker>; hx_sched.h Timeline). Copies at most `max_words` events (worker w's

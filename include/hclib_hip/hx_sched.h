@@ -258,6 +258,8 @@ struct SchedConfig {
                          // (PendingChunk) instead of behind a store round trip
     uint32_t dual = 1;   // kinds with process2 (KindDual): a wave holding more than 64
                          // items runs TWO per lane per batch, their bodies interleaved
+    uint32_t spills = 0; // hunger spills per batch at most (0: until the ring is below
+                         // spill_lo or no wave is hungry)
 };
 
 // Kind concept:
@@ -1084,6 +1086,9 @@ struct NarrowState {
     uint32_t ck, carry, top, tag, n_exec, n_spawn, batches;
 };
 
+#ifndef HX_PHASES
+#define HX_PHASES 0  // diagnostic: main-loop batch phase stamps (run_worker)
+#endif
 #ifndef HX_AFTER_BODY
 #define HX_AFTER_BODY 1
 #endif
@@ -1626,6 +1631,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     // batch loop's scalar state then spills less (v_writelane/readlane)
     uint32_t nbatch = 0, npush = 0, nsteal = 0;
     unsigned long long cyc_form = 0, cyc_proc = 0, cyc_push = 0;  // HX_STAMPS builds only
+    // HX_PHASES builds: main-loop single batches split at four s_memtime
+    // stamps: loop top -> pop issued -> pop landed -> body done -> batch end
+    unsigned long long ph_sum[4] = {0, 0, 0, 0}, ph_n = 0, ph_a = 0, ph_b = 0, ph_c = 0, ph_d = 0;
+    bool ph_single = false;
     uint32_t tag = 1;  // mark tags: 16 per batch
     for (int i = lane; i < kWaveSize; i += kWaveSize) st.mark[i] = 0;
     if (lane < 8) st.stolen_from[lane] = 0;
@@ -1892,6 +1901,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             continue;
         }
         ++nbatch;
+        if (HX_PHASES) {
+            ph_a = __builtin_amdgcn_s_memtime();
+            ph_single = false;
+        }
         // hunger signal: use the value loaded one batch ago (its latency hid
         // behind that whole batch), then issue the load for the next batch
         // (loaded every cfg.hunger batches; consumed that many batches later).
@@ -2004,6 +2017,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         int cnt = 0;
         unsigned long long ts0 = 0;
         if (HX_STAMPS && cfg.stamps) ts0 = __builtin_amdgcn_s_memtime();
+        if (HX_PHASES) {
+            ph_b = __builtin_amdgcn_s_memtime();
+            ph_single = true;
+        }
         // a batch of carried items only (take_ring == 0) loads nothing from
         // the ring: its idle lanes run (pure kinds) on a carried template
         if ((uint32_t)lane < carry || take_ring == 0) {
@@ -2019,6 +2036,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & M, tmpl);
         }
         carry = 0;
+        if (HX_PHASES) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            ph_c = __builtin_amdgcn_s_memtime();
+        }
         unsigned long long tsl = 0;
         if (HX_STAMPS && cfg.stamps) {
             // diagnostic build only: form = loop top + pop (LDS loads landed)
@@ -2037,6 +2058,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         // otherwise be scheduled after the publish, whose drain then waited
         // for those stores' whole round trip before the body)
         after_body<TW>(child);
+        if (HX_PHASES) {
+#pragma unroll
+            for (int i = 0; i < TW; ++i) asm volatile("" ::"v"(child[i]));
+            ph_d = __builtin_amdgcn_s_memtime();
+        }
         publish_pending<Kind, CAP>(pool, g, pend);
         if (HX_STAMPS && cfg.stamps) {
             const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
@@ -2139,6 +2165,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         if (sz > cfg.spill_hi || (hungry > 0 && sz >= lo)) {
             const unsigned long long ts = __builtin_amdgcn_s_memtime();
             const uint32_t cmax = pool.chunk;
+            uint32_t nsp = 0;
             while (sz > cfg.spill_hi || (hungry > 0 && sz >= lo)) {
                 uint32_t n = (sz + 1) / 2;
                 if (n > cmax) n = cmax;
@@ -2165,6 +2192,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 bot += n;
                 sz = top - bot;
                 if (hungry) --hungry;
+                if (cfg.spills && ++nsp >= cfg.spills && sz <= cfg.spill_hi) break;
             }
             lds_sum(st, 2, __builtin_amdgcn_s_memtime() - ts);
         }
@@ -2184,6 +2212,14 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             }
         }
         if (HX_STAMPS && cfg.stamps) t_batch = __builtin_amdgcn_s_memtime();
+        if (HX_PHASES && ph_single) {
+            const unsigned long long ph_e = __builtin_amdgcn_s_memtime();
+            ph_sum[0] += ph_b - ph_a;
+            ph_sum[1] += ph_c - ph_b;
+            ph_sum[2] += ph_d - ph_c;
+            ph_sum[3] += ph_e - ph_d;
+            ++ph_n;
+        }
     }
     publish_pending<Kind, CAP>(pool, g, pend);  // (error exits)
     if constexpr (WPG > 1) {
@@ -2260,6 +2296,11 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         case 20: v = n_narrow_in ? (unsigned long long)n_narrow : 0; break;
         case 21: v = n_narrow_in ? cyc_narrow : 0; break;
         case 22: v = n_narrow_in; break;
+        case 23: v = ph_n; break;
+        case 28: v = ph_sum[0]; break;
+        case 29: v = ph_sum[1]; break;
+        case 30: v = ph_sum[2]; break;
+        case 31: v = ph_sum[3]; break;
         case 24 + kCtrPushCycles - 4: v = c_push; break;
         case 24 + kCtrClockTicks - 4: v = t_end - t_begin; break;
         case 24 + kCtrRealTicks - 4: v = rt_end - rt_begin; break;
