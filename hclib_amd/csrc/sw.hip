@@ -1526,11 +1526,23 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
                      (T.corner_src ? 8ull : 0ull) | (T.left_lds ? 16ull : 0ull);
     }
     const int cget = (int)(uint32_t)cg;
+    // the LDS inputs, every load issued before any is used: read per element
+    // inside the conversion below, each load was a branch of its own and
+    // waited behind the previous element's store (the arrays may alias) —
+    // 0.9 us of a kept hop's 1.7 before its sweep (profiles/r05/sw_trace.json)
+    const lds_i32 *lsl = (const lds_i32 *)(T.left_lds ? T.left_lds : (const int *)top);
+    const lds_i32 *tsl = (const lds_i32 *)(T.top_lds ? T.top_lds : (const int *)top);
+    int lq[4], tq[KX];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lq[q] = lsl[T.left_lds ? rowq[q] - R0 - 1 : 0];
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+        const int x = lane + 64 * k;
+        tq[k] = tsl[T.top_lds && x < ncols ? x : 0];
+    }
     int lh[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-        lh[q] = T.left_lds ? *((const lds_i32 *)T.left_lds + (rowq[q] - R0 - 1))
-                           : (lglob ? (int)(uint32_t)lg[q] : -rowq[q]);
+    for (int q = 0; q < 4; ++q) lh[q] = T.left_lds ? lq[q] : (lglob ? (int)(uint32_t)lg[q] : -rowq[q]);
     // --- the left column as packed v
     const int base = (T.corner_src ? cget : T.corner_val) + R0 + C0;  // G(R0, C0)
     uint32_t l16[4];
@@ -1538,16 +1550,19 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
     for (int q = 0; q < 4; ++q) l16[q] = sw_f16_bits(lh[q] + rowq[q] + C0 - base);
     sw_h2 lr0 = sw_as_h2(l16[0] | (l16[2] << 16)), lr1 = sw_as_h2(l16[1] | (l16[3] << 16));
     // --- the top row as v (f16 in the low half), 0 past the tile
+    // (branch-free per element: selects, one predicated store)
+    const bool from_hin = T.hin != nullptr, top_known = T.hin != nullptr || T.top_lds != nullptr;
 #pragma unroll
     for (int k = 0; k < KX + 4; ++k) {
         const int x = lane + 64 * k;
-        if (x < topw) {
-            int v = 0;
-            if (k < KX && x < ncols)
-                v = T.hin ? (int)(uint32_t)th_[k] + R0 + (C0 + 1 + x) - base
-                          : (T.top_lds ? *((const lds_i32 *)T.top_lds + x) + R0 + (C0 + 1 + x) - base : -base);
-            top[x] = (int)sw_f16_bits(v);
+        int v = 0;
+        if (k < KX) {
+            const int src = from_hin ? (int)(uint32_t)th_[k] : tq[k];
+            const int vk = top_known ? src + R0 + (C0 + 1 + x) - base : -base;
+            v = x < ncols ? vk : 0;
         }
+        const int bits = (int)sw_f16_bits(v);
+        if (x < topw) top[x] = bits;
     }
     if (T.corner_lds) {
         // H(R0, C0 + ncols): the up tile's last bottom value (or the boundary)

@@ -880,7 +880,11 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // (scripts/sweep_uts.py: T1 1.37 -> 1.07 ms, T1XL 101 -> 97 ms, T3L even)
     // (fixed-shape GEO trees on 512-item rings every 64: T1XL 51.5 -> 49.9 ms,
     // T1L even, T2L slower; profiles/r02/geo_knobs.log)
-    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", geo_fixed && ring_used >= 512 ? 64 : 32);
+    // hunger read interval: 64 batches on fixed-shape 512-item rings and on
+    // BIN trees (T3L 29.34 -> 29.23 ms mean of 7 interleaved rounds, and
+    // -0.14 ms in two shorter sweeps: profiles/r05/sweep_h64sp1_t3l.log,
+    // sweep_wpg4_t3l.log, sweep_spills_t3l.log), 32 otherwise
+    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", (geo_fixed && ring_used >= 512) || bin ? 64 : 32);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
     cfg.backoff = (uint32_t)env_int("HCLIB_HIP_BACKOFF", 16);
     cfg.defer = (uint32_t)env_int("HCLIB_HIP_DEFER", 1);
