@@ -248,6 +248,8 @@ int finish_sched(SchedGlobals *host_copy, const char *who) {
         for (int i = 0; i < 3; ++i) host_copy->narrow[i] += r[20 + i];
         m.last_phase[0] += r[23];
         for (int i = 0; i < 4; ++i) m.last_phase[1 + i] += r[28 + i];
+        m.last_phase[5] += r[24];  // HX_PHASES builds only (else the stamps' push cycles)
+        m.last_phase[6] += r[27];
     }
     memcpy(m.last_counters, host_copy->counters, sizeof(m.last_counters));
     memcpy(m.last_narrow, host_copy->narrow, sizeof(m.last_narrow));

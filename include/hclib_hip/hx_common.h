@@ -85,9 +85,15 @@ __device__ __forceinline__ bool cas_sys(T *p, T expected, T desired) {
 // dwordx4 one. The load waits for itself (inline asm is invisible to the
 // compiler's waitcnt pass); ld_sc1_x4x2 issues two before one wait.
 typedef uint32_t hx_u32x4 __attribute__((ext_vector_type(4)));
+// The s_nop: a store of more than 8 bytes reads its data registers after
+// issue, and the compiler's hazard recognizer does not cover an inline-asm
+// store, so a VALU write of those registers right behind it (the next
+// store's address, built in the same registers) corrupted the stored data
+// (UTS T1: nodes lost and duplicated in 42 of 60 launches when the chunk
+// payload's reads moved ahead of its ticket and the schedule tightened)
 __device__ __forceinline__ void st_sc1_x4(void *p, uint4 v) {
     const hx_u32x4 x = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 2" ::"v"(p), "v"(x) : "memory");
 }
 __device__ __forceinline__ void ld_sc1_x4x2(const void *p, uint4 &a, uint4 &b) {
     hx_u32x4 x, y;

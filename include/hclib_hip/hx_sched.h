@@ -581,6 +581,17 @@ __device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &poo
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
     QueueHdr *h = &pool.hdr[q];
+    // lane i packs item bot+i as {template, k, kend} (n <= 64): its LDS reads
+    // go out before the ticket's round trip, which then hides them
+    const bool valid = (uint32_t)lane < n;
+    uint32_t w[W];
+    {
+        const uint32_t p = bot + (valid ? (uint32_t)lane : 0u);
+        const uint2 dd = st.d[p & (CAP - 1)];
+        load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & (CAP - 1), w);
+        w[W - 2] = dd.x;
+        w[W - 1] = dd.y & (kMaxChildren - 1);
+    }
     uint32_t pos = 0, seen = 0;
     int ok = 0;
     const bool fast = occ < pool.cap / 4;
@@ -620,16 +631,8 @@ __device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &poo
             __builtin_amdgcn_s_sleep(1);
         }
     }
-    // lane i packs item bot+i as {template, k, kend} (n <= 64)
     uint32_t *dst = pool.data + (size_t)slot * pool.chunk * W;
     {
-        const bool valid = (uint32_t)lane < n;
-        uint32_t w[W];
-        const uint32_t p = bot + (valid ? (uint32_t)lane : 0u);
-        const uint2 dd = st.d[p & (CAP - 1)];
-        load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & (CAP - 1), w);
-        w[W - 2] = dd.x;
-        w[W - 1] = dd.y & (kMaxChildren - 1);
         kind_export<Kind>(ctx, w, valid, &g->err);
         kind_trace_item<Kind>(ctx, w, valid, 2u, false);
         if (valid) {
@@ -1253,15 +1256,17 @@ __device__ bool inbox_put(const typename Kind::Ctx &ctx, Inbox<Kind> &ib, WaveSt
                           uint32_t n, SchedGlobals *g) {
     constexpr int W = Kind::kWords;
     const int lane = lane_id();
+    // the items' reads go out beside the claim (they depend on nothing it
+    // decides: one wait instead of three round trips in a row)
+    const bool valid = (uint32_t)lane < n;
+    const uint32_t p = bot + (valid ? (uint32_t)lane : 0u);
+    const uint2 dd = st.d[p & (CAP - 1)];
     uint32_t ok = 0;
     if (lane == 0) ok = lds_cas(&ib.state, 0u, 2u) ? 1u : 0u;
+    uint32_t w[W];
+    load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & (CAP - 1), w);
     if (!lane0(ok)) return false;
     {
-        const bool valid = (uint32_t)lane < n;
-        const uint32_t p = bot + (valid ? (uint32_t)lane : 0u);
-        const uint2 dd = st.d[p & (CAP - 1)];
-        uint32_t w[W];
-        load_tmpl<Kind, CAP>(st, (p - (dd.y >> 24)) & (CAP - 1), w);
         w[W - 2] = dd.x;
         w[W - 1] = dd.y & (kMaxChildren - 1);
         kind_export<Kind>(ctx, w, valid, &g->err);
@@ -1633,7 +1638,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     unsigned long long cyc_form = 0, cyc_proc = 0, cyc_push = 0;  // HX_STAMPS builds only
     // HX_PHASES builds: main-loop single batches split at four s_memtime
     // stamps: loop top -> pop issued -> pop landed -> body done -> batch end
-    unsigned long long ph_sum[4] = {0, 0, 0, 0}, ph_n = 0, ph_a = 0, ph_b = 0, ph_c = 0, ph_d = 0;
+    unsigned long long ph_sum[6] = {0, 0, 0, 0, 0, 0}, ph_n = 0, ph_a = 0, ph_b = 0, ph_c = 0, ph_d = 0, ph_m = 0,
+                       ph_p = 0;
     bool ph_single = false;
     uint32_t tag = 1;  // mark tags: 16 per batch
     for (int i = lane; i < kWaveSize; i += kWaveSize) st.mark[i] = 0;
@@ -2148,6 +2154,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 continue;
             }
         }
+        if (HX_PHASES) ph_m = __builtin_amdgcn_s_memtime();
         if (!make_room(tout)) break;  // error already recorded
         if (uniform) {
             push_uniform<Kind, CAP>(st, top, excl, tout, mu, nch != 0, child);
@@ -2158,6 +2165,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         top += tout;
         if (HX_STAMPS && cfg.stamps) cyc_push += __builtin_amdgcn_s_memtime() - ts0;
         }  // single batch
+        if (HX_PHASES) ph_p = __builtin_amdgcn_s_memtime();
         // ---- give the oldest items to hungry waves, or relieve a full ring
         uint32_t sz = top - bot;
         uint32_t hungry = cfg.nwaves > outst ? cfg.nwaves - outst : 0;
@@ -2173,12 +2181,18 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 // home deque first, then the other deques of this XCD slice
                 bool ok = false;
                 if constexpr (WPG > 1) {
-                    // an idle sibling of this workgroup first (LDS, no HBM round trip)
-                    for (uint32_t a = 1; a < (uint32_t)WPG && !ok; ++a) {
-                        Inbox<Kind> &sib = ib[(wave + a) % (uint32_t)WPG];
-                        if (lane0(lds_load(&sib.idle)) == 1u && lane0(lds_load(&sib.state)) == 0u)
-                            ok = inbox_put<Kind, CAP>(ctx, sib, st, bot, n, g);
+                    // an idle sibling of this workgroup first (LDS, no HBM
+                    // round trip); every sibling's flags read in one go
+                    uint32_t sid[WPG], sst[WPG];
+#pragma unroll
+                    for (uint32_t a = 1; a < (uint32_t)WPG; ++a) {
+                        sid[a] = lds_load(&ib[(wave + a) % (uint32_t)WPG].idle);
+                        sst[a] = lds_load(&ib[(wave + a) % (uint32_t)WPG].state);
                     }
+#pragma unroll
+                    for (uint32_t a = 1; a < (uint32_t)WPG; ++a)
+                        if (!ok && lane0(sid[a]) == 1u && lane0(sst[a]) == 0u)
+                            ok = inbox_put<Kind, CAP>(ctx, ib[(wave + a) % (uint32_t)WPG], st, bot, n, g);
                 }
                 if (!ok) publish_pending<Kind, CAP>(pool, g, pend);  // one deferred chunk at a time
                 // where the chunk goes: the home deque first, then the XCD's others
@@ -2218,6 +2232,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             ph_sum[1] += ph_c - ph_b;
             ph_sum[2] += ph_d - ph_c;
             ph_sum[3] += ph_e - ph_d;
+            ph_sum[4] += ph_m - ph_d;  // body -> push begins (carry decision, publish)
+            ph_sum[5] += ph_p - ph_m;  // the push
             ++ph_n;
         }
     }
@@ -2301,10 +2317,10 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         case 29: v = ph_sum[1]; break;
         case 30: v = ph_sum[2]; break;
         case 31: v = ph_sum[3]; break;
-        case 24 + kCtrPushCycles - 4: v = c_push; break;
+        case 24 + kCtrPushCycles - 4: v = HX_PHASES ? ph_sum[4] : c_push; break;
         case 24 + kCtrClockTicks - 4: v = t_end - t_begin; break;
         case 24 + kCtrRealTicks - 4: v = rt_end - rt_begin; break;
-        case 24 + kCtrFormCycles - 4: v = c_form; break;
+        case 24 + kCtrFormCycles - 4: v = HX_PHASES ? ph_sum[5] : c_form; break;
         default: break;
         }
         if (lane < kWaveCtrWords) g->wave_ctr[(size_t)gid * kWaveCtrWords + lane] = v;

@@ -23,6 +23,7 @@ for name in sys.argv[1:] or ["T3L", "T1XL"]:
     c = H.last_sched_counters()
     print(json.dumps({"tree": name, "kernel_ms": round(r["kernel_ms"], 3), "main_batches": p[0],
                       "cycles_per_main_batch": {"top_to_pop": round(p[1] / n), "pop": round(p[2] / n),
-                                                "body": round(p[3] / n), "push_spill": round(p[4] / n)},
+                                                "body": round(p[3] / n), "push_spill": round(p[4] / n),
+                                                "of_which_to_push": round(p[5] / n), "of_which_push": round(p[6] / n)},
                       "spill_section_cycles_per_main_batch": round(c[11] / n), "chunks_pushed": r["chunks_pushed"],
                       "narrow_batches": nb, "narrow_cycles_per_batch": round(ncyc / max(1, nb))}), flush=True)
