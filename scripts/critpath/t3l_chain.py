@@ -42,7 +42,7 @@ def analyse(r, raw):
     fill = ((info >> np.uint64(20)) & np.uint64(0x7f)).astype(np.int64)
     step = np.diff(t)  # step[i]: chain node i+1 ran at t[i], its child at t[i+1]
     same = wid[1:] == wid[:-1]
-    wpg = int(os.environ.get("HCLIB_HIP_WPG", "2"))
+    wpg = int(H.uts_last_launch()["workers_per_group"])
     sib = (~same) & ((wid[1:] // wpg) == (wid[:-1] // wpg))
     far = (~same) & (~sib)
     nx, dx = narrow[1:], dual[1:]
