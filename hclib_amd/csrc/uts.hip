@@ -802,7 +802,11 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     ctx.nb = d_nb;
 
     PoolView pool;
-    const uint32_t nq = (uint32_t)env_int("HCLIB_HIP_DEQUES", 64);
+    // 128 chunk deques (8 per XCD slice of 16): T3L 28.64 -> 28.57 ms and
+    // 28.73 -> 28.58, T1XL 31.19 -> 31.00, T1 0.206 -> 0.202 (means of
+    // interleaved rounds, profiles/r05/sweep_dq_*.log, sweep_t3l_j.log); 32
+    // is a millisecond slower on T3L
+    const uint32_t nq = (uint32_t)env_int("HCLIB_HIP_DEQUES", 128);
     HX_TRY(make_pool(nq, (uint32_t)env_int("HCLIB_HIP_DEQUE_CAP", 4096),
                      (uint32_t)env_int("HCLIB_HIP_CHUNK", 64), UtsKind<kUtsBin, 0>::kWords, &pool));
     const bool bin = params->type == 0 && T.rules.size() == 2 && T.rules[1].x == 1 && T.stationary;
