@@ -884,16 +884,19 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // (scripts/sweep_uts.py: T1 1.37 -> 1.07 ms, T1XL 101 -> 97 ms, T3L even)
     // (fixed-shape GEO trees on 512-item rings every 64: T1XL 51.5 -> 49.9 ms,
     // T1L even, T2L slower; profiles/r02/geo_knobs.log)
-    // hunger read interval: 64 batches on fixed-shape 512-item rings and on
-    // BIN trees (T3L 29.34 -> 29.23 ms mean of 7 interleaved rounds, and
+    // hunger read interval: 64 batches on BIN trees (T3L 29.34 -> 29.23 ms mean of 7 interleaved rounds, and
     // -0.14 ms in two shorter sweeps: profiles/r05/sweep_h64sp1_t3l.log,
     // sweep_wpg4_t3l.log, sweep_spills_t3l.log), 32 otherwise
     // ... except small fixed-shape trees (expected < 3e7 nodes), which run
     // a few dozen batches per wave: 32 (T1 0.210 -> 0.200-0.201 ms mean of 6
     // and 8 interleaved rounds; T1L wants 64: 2.44 vs 2.48 ms;
     // profiles/r05/sweep_t1_g.log, sweep_t1_h.log, sweep_t1l_h.log)
+    // ... and large fixed-shape trees every 128 (T1XL 31.15 -> 30.77 ms, T1L
+    // 2.417 -> 2.383, means of 4-5 interleaved rounds, sweep_t1xl_l.log,
+    // sweep_t1l_l.log)
     const bool small_fixed = geo_fixed && uts_expected_nodes(*params) < 3e7;
-    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", ((geo_fixed && ring_used >= 512) || bin) && !small_fixed ? 64 : 32);
+    const bool large_fixed = geo_fixed && ring_used >= 512 && !small_fixed;
+    cfg.hunger = (uint32_t)env_int("HCLIB_HIP_HUNGER", large_fixed ? 128 : bin ? 64 : 32);
     cfg.carry = (uint32_t)env_int("HCLIB_HIP_CARRY", 2);
     cfg.backoff = (uint32_t)env_int("HCLIB_HIP_BACKOFF", 16);
     cfg.defer = (uint32_t)env_int("HCLIB_HIP_DEFER", 1);

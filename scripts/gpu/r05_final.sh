@@ -8,6 +8,7 @@ OUT=gpurun_out/r05f
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/full_tests.log 2>&1 &&
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")" > $OUT/smoke.log 2>&1 &&
 timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err &&
 rm -rf $OUT/prof &&
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u bench.py > $OUT/bench_prof.json 2> $OUT/bench_prof.err &&
