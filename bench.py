@@ -475,18 +475,115 @@ def sharded_sw(H, rank, world, be, steps=2):
     return out
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(argv, n, cmd=None, timeout_s=None, grace_s=60.0, out=None):
+    """`python bench.py --gpus N` with no launcher around it (WORLD_SIZE
+    unset): start N fresh rank processes (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set, one GPU each), wait for all of them, re-print rank 0's JSON
+    line and return the worst exit status. This process never imports torch
+    or touches the GPU and never execs: the ranks are children. If a rank
+    fails, the others get `grace_s` to finish (a rank that lost its peer sits
+    in a collective until the group timeout) and are then killed; the whole
+    job is bounded by `timeout_s` (HCLIB_BENCH_LAUNCH_TIMEOUT_S, 3600 s).
+    `cmd` (tests) replaces [python, bench.py]; `out` receives the line.
+    The reference's distributed UTS is launched the same way, one process per
+    PE by its launcher (test/performance-regression/full-apps/uts/
+    uts_hclib_shmem_opt.cpp:98-140)."""
+    import signal
+    import subprocess
+    import threading
+
+    out = out or sys.stdout
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("HCLIB_BENCH_LAUNCH_TIMEOUT_S", "3600"))
+    cmd = cmd or [sys.executable, "-u", os.path.abspath(__file__)]
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        # rank 0's stdout is read here (its JSON line); the others' stdout
+        # goes to this process's stderr, so stdout carries one line only
+        procs.append(subprocess.Popen(cmd + list(argv), env=env, stdout=subprocess.PIPE if r == 0 else 2,
+                                      start_new_session=True))
+    line = [None]
+
+    def read_rank0():
+        for raw in procs[0].stdout:
+            s = raw.decode(errors="replace").rstrip("\n")
+            try:
+                obj = json.loads(s)
+            except ValueError:
+                obj = None
+            if isinstance(obj, dict) and "metric" in obj:
+                line[0] = obj
+            else:
+                print(s, file=sys.stderr, flush=True)
+    reader = threading.Thread(target=read_rank0, daemon=True)
+    reader.start()
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)  # the rank's own session (start_new_session)
+                except OSError:
+                    pass
+    t0 = time.monotonic()
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        now = time.monotonic()
+        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
+            failed_at = now
+            log(f"self_launch: rank(s) {[i for i, p in enumerate(procs) if p.poll() not in (None, 0)]} failed; "
+                f"the others get {grace_s:g} s")
+        if (failed_at is not None and now - failed_at > grace_s) or now - t0 > timeout_s:
+            log("self_launch: killing the remaining ranks")
+            kill_all()
+            break
+        time.sleep(0.05)
+    codes = [p.wait() for p in procs]
+    reader.join(5.0)
+    if line[0] is not None:
+        line[0]["launcher"] = f"bench.py self-launch: {n} rank processes, MASTER 127.0.0.1:{port}"
+        print(json.dumps(line[0]), file=out, flush=True)
+    # worst status: a signal (negative code) as 128 + signal, as a shell reports it
+    worst = 0
+    for c in codes:
+        c = 128 - c if c < 0 else c
+        worst = max(worst, c)
+    if line[0] is None and worst == 0:
+        worst = 1  # every rank exited 0 but rank 0 printed no line
+    return worst
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--split", type=int, default=64, help="replicated top levels before sharding")
+    ap.add_argument("--split", type=int, default=1,
+                    help="depth at which T3L's nodes are hashed to ranks (the levels above are replicated)")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--backend", default="nccl",
                     help="collective backend (nccl = RCCL; gloo only for rehearsals)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses device 0 (with --backend gloo)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: become one (before any torch / HIP call)
+        sys.exit(self_launch(sys.argv[1:], args.gpus))
 
     import torch  # noqa: F401  (one HIP runtime for torch + the module)
 
@@ -583,7 +680,8 @@ def main():
         "dtype": "u32",
         "data": "synthetic (UTS trees are generated from their published parameters; no dataset)",
         "config": {
-            "workload": f"test/uts T3L ({T3L}) sharded over {world} GPU(s), split depth {args.split}",
+            "workload": (f"test/uts T3L ({T3L}) sharded over {world} GPUs, split depth {args.split}" if world > 1
+                         else f"test/uts T3L ({T3L}) searched whole on 1 GPU (no split)"),
             "nodes": T3L_GOLD[0],
             "bit_exact": True,
             "uts_kernel_ms_rank0": sum(kernel_ms) / len(kernel_ms),

@@ -36,10 +36,7 @@ CFLAGS = [
 
 
 VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "trace": ["-DHX_TRACE=1"], "timeline": ["-DHX_TIMELINE=1"],
-            # SW band-sweep timing experiments (wrong results by design: sw.hip HX_SW_EXP)
-            "pkexp1": ["-DHX_SW_PK_EXP=1"], "pk1w": ["-DHX_PK1W=1"], "untag": ["-DHX_UNTAG=1"], "pf1": ["-DHX_SW_PK_PF=1"], "pf2": ["-DHX_SW_PK_PF=2"], "pkexp2": ["-DHX_SW_PK_EXP=2"],
-            "swexp1": ["-DHX_SW_EXP=1"], "swexp2": ["-DHX_SW_EXP=2"], "swexp3": ["-DHX_SW_EXP=3"], "swexp4": ["-DHX_SW_EXP=4"],
-            "shift": ["-DHX_SW_SHIFT=1"], "strict": ["-DHX_STRICT_HANDOFF=1"],
+            "strict": ["-DHX_STRICT_HANDOFF=1"],
             "narrow_noinline": ["-DHX_NARROW_NOINLINE=1"], "carry_perm": ["-DHX_CARRY_LDS=0"], "base": [], "nohoist": ["-DHX_CARRY_HOIST=0"], "fib_small": ["-DHX_FIB_CAP=512", "-DHX_FIB_SCOPES=256", "-DHX_FIB_PIECES=2"],
             "sched_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
             "sched_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],

@@ -90,21 +90,6 @@ __device__ __forceinline__ int shift_up1(int v) {
 #ifndef HX_STAMPS
 #define HX_STAMPS 0
 #endif
-// Timing experiments on the band sweep (diagnostic builds only, results are
-// wrong by design): 1 = lanes 0..62 skip their dummy ring writes (exec-masked
-// store by lane 63 alone), 2 = no top-ring loads (lane 0's up value is a
-// constant), 3 = no code loads (a constant score row)
-#ifndef HX_SW_EXP
-#define HX_SW_EXP 0
-#endif
-// 64-step band hand-offs gather lane 63's outputs by DPP (1) or store them
-// to the ring every step from every lane (0, default). Measured same-box
-// (profiles/r03/sw_shift_ab.log): the one-tile-row sweep 57 -> 55 cycles per
-// step at R = 2 (48 -> 45 at R = 1), but the DAG 8.12 -> 8.55 ms (its
-// consumer wave receives each chunk in one burst at the chunk's end)
-#ifndef HX_SW_SHIFT
-#define HX_SW_SHIFT 0
-#endif
 __device__ __forceinline__ unsigned long long sw_stamp() {
 #if HX_STAMPS
     unsigned long long t;
@@ -580,8 +565,8 @@ constexpr int kSwRingStride = kSwRing + 4;
 constexpr int kSwSub = 16;    // steps per hand-off
 // dummy ring slots per compute wave (its lanes 0..62 write there every step
 // while lane 63 writes the out ring; lane stride 1: neighbours' two-dword
-// writes overlap. HX_SW_EXP 4: stride 2, no overlap)
-constexpr int kSwDummy = HX_SW_EXP == 4 ? 256 : 128;
+// writes overlap, which measured no slower than stride 2)
+constexpr int kSwDummy = 128;
 
 __host__ __device__ inline size_t sw_band_lds_bytes(int nw) {
     return (size_t)(nw + 1) * kSwRingStride * 4  // rings
@@ -705,9 +690,8 @@ __device__ __forceinline__ void sw_band_subR(int s, int ncols, const int *top4, 
                                              const uint32_t (&mrow)[R], int (&lr)[R], int &diag, int &acc) {
     constexpr int G = K / 4;
     const int lane = lane_id();
-    int4 tn = HX_SW_EXP == 2 ? make_int4(s, s, s, s) : *(const int4 *)top4,
-         tn2 = HX_SW_EXP == 2 ? tn : *(const int4 *)(top4 + 4);
-    uint32_t cn = HX_SW_EXP == 3 ? 0x01020300u : code4[0], cn2 = HX_SW_EXP == 3 ? cn : code4[1];
+    int4 tn = *(const int4 *)top4, tn2 = *(const int4 *)(top4 + 4);
+    uint32_t cn = code4[0], cn2 = code4[1];
 #pragma unroll
     for (int m = 0; m < G; ++m) {
         const int4 tc = tn;
@@ -715,8 +699,8 @@ __device__ __forceinline__ void sw_band_subR(int s, int ncols, const int *top4, 
         tn = tn2;
         cn = cn2;
         if (m + 2 < G) {
-            if (HX_SW_EXP != 2) tn2 = *(const int4 *)(top4 + 4 * (m + 2));
-            if (HX_SW_EXP != 3) cn2 = code4[m + 2];
+            tn2 = *(const int4 *)(top4 + 4 * (m + 2));
+            cn2 = code4[m + 2];
         }
         uint32_t sc[R];
 #pragma unroll
@@ -740,7 +724,7 @@ __device__ __forceinline__ void sw_band_subR(int s, int ncols, const int *top4, 
             }
             diag = MASK ? (v ? up0 : diag) : up0;
             if (SHIFT) acc = __builtin_amdgcn_update_dpp(lr[R - 1], acc, 0x130, 0xf, 0xf, false);
-            else if (HX_SW_EXP != 1 || lane == 63) wb[k] = lr[R - 1];
+            else wb[k] = lr[R - 1];
         }
     }
 }
@@ -940,7 +924,7 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
         mr[q] = sw_row2(c.s2[r - 1 + q]);
         lr[q] = left_h(r + q) + (r + q) + C0;
     }
-    int *wbase = lane == 63 ? ring_out : dummy + w * kSwDummy + (HX_SW_EXP == 4 ? 2 * lane : lane);
+    int *wbase = lane == 63 ? ring_out : dummy + w * kSwDummy + lane;
     const int8_t *s1 = c.s1 + C0;
     // s1 code (1..4) of column x; loads clamped to the band, never predicated,
     // so that nothing waits for them before their use
@@ -959,9 +943,10 @@ __device__ bool sw_band_row(const SwCtx &c, const SwBand &B, int w, int *rings, 
     const int cofs = (S * lane) & 3;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = true;
-    // 64-step hand-offs with one row of skew: lane 63's outputs gathered by
-    // DPP (sw_band_sub SHIFT) and stored once per chunk
-    constexpr bool kShift = K == 64 && S == 1 && HX_SW_SHIFT;
+    // (SHIFT, lane 63's outputs gathered by DPP and stored once per 64-step
+    // chunk: the one-tile-row sweep 57 -> 55 cycles per step, but the DAG
+    // 8.12 -> 8.55 ms, profiles/r03/sw_shift_ab.log; not built)
+    constexpr bool kShift = false;
     int acc = 0;
     // (trace builds: the loop start only — a stamp inside the loop, an SMEM
     // read, waits for every LDS operation in flight and slows the sweep)
@@ -1342,15 +1327,9 @@ struct SwPkTile {
 // uint4 {sc0(2p), sc1(2p), sc0(2p+1), sc1(2p+1)}. misc[5] = chunks written,
 // misc[6] = chunks read (both reset between tiles).
 constexpr int kSwPkSlots = 2;
-#ifndef HX_SW_PK_PF
-#define HX_SW_PK_PF 3  // sweep operand prefetch distance (groups of 4 steps)
-#endif
-// Timing experiments (diagnostic builds only, results wrong by design):
-// 1 = the score wave computes chunk 0 only and then just publishes the rest,
-// 2 = the sweep wave reads no ring (constant scores)
-#ifndef HX_SW_PK_EXP
-#define HX_SW_PK_EXP 0
-#endif
+// the sweep's operand prefetch distance (groups of 4 steps; 1-3 measured
+// flat, profiles/r03/sw_pk_prefetch_ab.log)
+constexpr int kSwPkPf = 3;
 constexpr int kSwPkRingU4 = kSwPkSlots * 32 * 64;  // uint4 entries
 // LDS: ring | top | sel x 4 | right columns [2][256] | misc[16] | score rows [4][64] | next top row [512]
 constexpr int kSwPkMisc = 16;
@@ -1449,7 +1428,7 @@ __device__ bool sw_pk_scores(const SwCtx &c, int ncols, uint4 *ring, const int *
         uint4 *dst = ring + (size_t)((k % kSwPkSlots) * 32) * 64 + lane;
         const int *sp = selp + 64 * k;
 #pragma unroll
-        for (int g = 0; g < 16 && (HX_SW_PK_EXP != 1 || k == 0); ++g) {
+        for (int g = 0; g < 16; ++g) {
             const int4 sv = *(const int4 *)(sp + 4 * g);
             dst[(2 * g) * 64] = make_uint4(__builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv.x),
                                            __builtin_amdgcn_perm(mhi1, mlo1, (uint32_t)sv.x),
@@ -1595,18 +1574,13 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
         const uint4 *src = ring + (size_t)((k % kSwPkSlots) * 32) * 64 + lane;
         uint32_t acc = 0;
         // operands of group g + kPf are loaded while group g computes
-        constexpr int kPf = HX_SW_PK_PF;
+        constexpr int kPf = kSwPkPf;
         int4 tq[kPf + 1];
         uint4 rq0[kPf + 1], rq1[kPf + 1];
         auto load_group = [&](int g) {
             tq[g % (kPf + 1)] = *(const int4 *)(top + s0 + 4 * g);
-            if (HX_SW_PK_EXP == 2) {
-                rq0[g % (kPf + 1)] = make_uint4(g, 2 * g, g, 2 * g);
-                rq1[g % (kPf + 1)] = make_uint4(3 * g, g, 3 * g, g);
-            } else {
-                rq0[g % (kPf + 1)] = src[(2 * g) * 64];
-                rq1[g % (kPf + 1)] = src[(2 * g + 1) * 64];
-            }
+            rq0[g % (kPf + 1)] = src[(2 * g) * 64];
+            rq1[g % (kPf + 1)] = src[(2 * g + 1) * 64];
         };
 #pragma unroll
         for (int g = 0; g < kPf; ++g) load_group(g);

@@ -232,6 +232,9 @@ struct UtsKind {
                                                  uint32_t *child, uint32_t *err, bool valid) {
         const int h1 = (int)(F == 3 ? t[5] & 0x7fffffffu : t[5]) + 1;
         bool counted = valid;
+        // (the worker loop filters only where the seeding cannot reach the
+        // split; a wave-uniform branch around this was no faster: the FEAT
+        // = 1 body's cost is its code generation, profiles/r06/shard_big_a.log)
         if (F && c.nshards > 1) {
             if (h1 == c.split && (ch[0] % (uint32_t)c.nshards) != (uint32_t)c.shard) return 0;
             if (h1 < c.split && c.shard != 0) counted = false;
@@ -825,6 +828,16 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     const bool global = nshards > 1 && m.gview.hdr != nullptr && max_levels == 0;
     // fixed-shape trees start seeded (breadth-first, hx_sched.h seed_levels)
     const bool seed_on = geo_fixed && !global && env_int("HCLIB_HIP_UTS_SEED", 1);
+    // BIN shards: the grid expands the replicated top levels breadth-first to
+    // the split depth (hx_sched.h seed_levels, the shard filter inside the
+    // seeding) and then runs the plain kernel of a whole-tree search. With
+    // the filter in the worker loop instead (FEAT = 1) the shard holding
+    // T3L's deep chain ran 2.3-2.7 ms slower than the whole tree, although
+    // below the split the filter executes nothing: the FEAT = 1 body
+    // compiles the span-bound narrow loop worse (the FEAT = 0 kernel on the
+    // same shard: +0.05-0.14 ms; profiles/r06/shard_big_a.log)
+    const bool bin_seed = bin && nshards > 1 && !global && max_levels == 0 && split_depth >= 1 &&
+                          split_depth + 1 < kSeedMaxLevels && env_int("HCLIB_HIP_UTS_SEED", 1);
     // BIN trees: four worker waves per CU in one workgroup (one per SIMD;
     // three siblings to hand work to through LDS before the HBM deques):
     // T3L 29.08 -> 28.76 ms mean of 6 interleaved rounds against two per CU
@@ -941,6 +954,12 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
                               n_split <= 0.5 * cap && n_next / nshards <= (double)grid * (512 / 8);
             seed.min_levels = fits ? (uint32_t)split_depth : 0u;
         }
+    } else if (bin_seed) {
+        // exactly the split's levels: a BIN level holds ~b0 slots (critical
+        // branching, sd ~ sqrt(b0 d m^2 q (1 - q))), far inside the buffer
+        seed.target = 1;
+        seed.max_levels = (uint32_t)split_depth;
+        seed.min_levels = (uint32_t)split_depth;
     }
     HX_TRY(reset_sched(pool, 1, global, (uint32_t)grid, seed.target ? &seed : nullptr));
     HX_HIP(hipEventRecord(m.ev0, m.stream));
@@ -977,10 +996,12 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
             k_uts_search<kUtsBin, 1, 1024, true>, k_uts_search<kUtsGeoFixed, 1, 512, true>};
         kern = gkernels[mode];
     }
-    if (mode == kUtsGeoFixed && !feat) {  // ring-size variants of the fixed-shape GEO search
-        const int ring = env_int("HCLIB_HIP_UTS_RING", ring_default);
-        if (ring == 256) kern = k_uts_search<kUtsGeoFixed, 0, 256>;
-        else if (ring == 1024) kern = k_uts_search<kUtsGeoFixed, 0, 1024>;
+    // ring-size variants of the fixed-shape GEO search: whole-tree launches
+    // only (ring_used: sharded and histogram launches size spill_lo and the
+    // seeding's fit check for 512-item rings)
+    if (mode == kUtsGeoFixed && !feat && !global) {
+        if (ring_used == 256) kern = k_uts_search<kUtsGeoFixed, 0, 256>;
+        else if (ring_used == 1024) kern = k_uts_search<kUtsGeoFixed, 0, 1024>;
     }
     // BIN trees: the worker waves of a CU share a workgroup and hand work
     // to each other through LDS before the HBM deques (two: T3L 34.0 ->
@@ -998,10 +1019,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     }
     {
         int ring_k = mode == kUtsBin ? 1024 : 512;
-        if (mode == kUtsGeoFixed && !feat && !global) {
-            const int ring = env_int("HCLIB_HIP_UTS_RING", ring_default);
-            if (ring == 256 || ring == 1024) ring_k = ring;
-        }
+        if (mode == kUtsGeoFixed && !feat && !global && (ring_used == 256 || ring_used == 1024)) ring_k = ring_used;
         g_last_launch = hclib_hip_uts_launch_t{mode, trace ? 1 + trace_kind : (feat || global ? 1 : 0), wpg, grid, ring_k,
                                                seed.target ? 1 : 0, (int)seed.target, (int)cfg.spill_lo,
                                                grid / (m.num_cus > 0 ? m.num_cus : 1)};

@@ -429,11 +429,6 @@ def sw_exchange(make_job, rank: int, world: int, backend: str, expected, steps: 
             return None
         return check
 
-    def sync():
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-        dist.barrier(group=ctrl)
-
     def maxr(x):
         t = torch.tensor([float(x)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctrl)
@@ -443,11 +438,37 @@ def sw_exchange(make_job, rank: int, world: int, backend: str, expected, steps: 
         group = dist.new_group(backend=xb)  # collective; a fresh group per attempt
         err = None
         best = None
-        try:
-            for _ in range(steps):
+
+        def fail(e):
+            nonlocal err
+            err = f"rank {rank}: {type(e).__name__}: {str(e)[:200]}"
+            if not isinstance(e, ExchangeAborted):
+                try:
+                    store.set(k, err)
+                except Exception:  # noqa: BLE001
+                    pass
+
+        def agreed_ok():
+            # the one collective every rank reaches at every point below, so a
+            # rank that failed anywhere and a rank that did not issue the same
+            # collective on ctrl (a failed rank never sits in a barrier while
+            # its peer is in an all-reduce); it doubles as the barrier
+            return maxr(1.0 if (err or abort_of(k)()) else 0.0) == 0.0
+
+        ok = True
+        for _ in range(steps):
+            job = None
+            try:
                 job = make_job(xb, group, abort_of(k))
-                sync()
-                t0 = time.perf_counter()
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001 (agreed on at once, below)
+                fail(e)
+            if not agreed_ok():
+                ok = False
+                break
+            t0 = time.perf_counter()
+            try:
                 score, tiles = job.run()
                 if torch.cuda.is_available():
                     torch.cuda.synchronize()
@@ -455,15 +476,12 @@ def sw_exchange(make_job, rank: int, world: int, backend: str, expected, steps: 
                 if (score, tiles) != tuple(expected):
                     raise RuntimeError(f"mismatch: score {score}, tiles {tiles}, want {tuple(expected)}")
                 best = ms if best is None else min(best, ms)
-        except Exception as e:  # noqa: BLE001 (agreed on below, every rank reaches the control group)
-            err = f"rank {rank}: {type(e).__name__}: {str(e)[:200]}"
-            if not isinstance(e, ExchangeAborted):
-                try:
-                    store.set(k, err)
-                except Exception:  # noqa: BLE001
-                    pass
-        failed = maxr(1.0 if (err or abort_of(k)()) else 0.0) != 0.0
-        if failed:
+            except Exception as e:  # noqa: BLE001
+                fail(e)
+            if not agreed_ok():
+                ok = False
+                break
+        if not ok:
             if xb == "nccl":
                 # kernels of the failed exchange may still wait on the band's
                 # stream: abort the communicator so they end (best effort)

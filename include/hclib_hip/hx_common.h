@@ -90,7 +90,10 @@ typedef uint32_t hx_u32x4 __attribute__((ext_vector_type(4)));
 // store, so a VALU write of those registers right behind it (the next
 // store's address, built in the same registers) corrupted the stored data
 // (UTS T1: nodes lost and duplicated in 42 of 60 launches when the chunk
-// payload's reads moved ahead of its ticket and the schedule tightened)
+// payload's reads moved ahead of its ticket and the schedule tightened).
+// RULE for every inline-asm store of dwordx3 / dwordx4 in this tree: the
+// same asm statement ends the store with `s_nop N`, N >= 1, right after it
+// (tests/test_asm_hazards.py enforces it on the CPU suite)
 __device__ __forceinline__ void st_sc1_x4(void *p, uint4 v) {
     const hx_u32x4 x = {v.x, v.y, v.z, v.w};
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 2" ::"v"(p), "v"(x) : "memory");

@@ -1505,7 +1505,10 @@ __device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Ac
         }
         // every level's slots land before the result is published, on every
         // broadcast line (1,023 waves polling one line made it a hot spot:
-        // the first grid-wide level took 20 us, timeline tl_t1_a)
+        // the first grid-wide level took 20 us, timeline tl_t1_a). The slot
+        // stores are inline-asm sc1 stores the waitcnt pass cannot see, so
+        // they are drained here, before the publish, unconditionally
+        vm_drain();
         if (HX_SEED_FENCES) release_agent();
         for (uint32_t i = (uint32_t)lane; i < (uint32_t)kSeedGoLines; i += 64) {
             // one 8-byte store {size + 1, depth}: a reader that sees the size sees the depth
