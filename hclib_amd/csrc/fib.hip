@@ -327,6 +327,9 @@ extern "C" int hclib_hip_fib(int n, int64_t *value, hclib_hip_fib_result_t *resu
     cfg.spill_hi = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_HI", seed_pw > 0 ? 320 : 256);
     // scripts/sweep_uts.py fib30 (profiles/r01_s5/knob_sweeps.log): 32 -> 1.50 ms, 2 -> 1.70 ms
     cfg.spill_lo = (uint32_t)env_int("HCLIB_HIP_FIB_SPILL_LO", seed_pw > 0 ? 64 : 32);
+    // seeded fib: its first batches see every wave busy, as the host set it
+    // (fib(30) 0.40 -> 0.39 ms, profiles/r06/ab_outstpf.log)
+    cfg.hunger_init_full = 1;
     cfg.spin_limit = (uint32_t)env_int("HCLIB_HIP_SPIN_LIMIT_MS", 20000);
     cfg.nwaves = (uint32_t)grid;
     cfg.stamps = (uint32_t)env_int("HCLIB_HIP_STAMPS", 0);

@@ -260,6 +260,11 @@ struct SchedConfig {
                          // items runs TWO per lane per batch, their bodies interleaved
     uint32_t spills = 0; // hunger spills per batch at most (0: until the ring is below
                          // spill_lo or no wave is hungry)
+    // a seeded launch's first batches run before any hunger read has landed:
+    // 0 = they see every wave hungry (an early rebalancing of the seeded
+    // shares, from spill_lo items), 1 = they see none hungry (every wave holds
+    // its share)
+    uint32_t hunger_init_full = 0;
 };
 
 // Kind concept:
@@ -1722,7 +1727,13 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     }
     unsigned long long t_batch = t_mark;  // cfg.stamps only
     bool busy_phase = true;
-    uint32_t outst_pf = 0;  // lane 0: `outstanding` as loaded one batch ago
+    // lane 0: `outstanding` as loaded one batch ago. Until the first load
+    // lands it reads 0, "every wave hungry": true for an unseeded launch (one
+    // busy wave), and for a seeded one (every wave busy) an early rebalancing
+    // of the seeded shares, which measured faster on the GEO trees (T1 0.20 vs
+    // 0.22-0.23 ms, T1XL 30.8 vs 31.5) and slower on fib (0.40 vs 0.39 ms):
+    // cfg.hunger_init_full picks (profiles/r06/ab_outstpf.log)
+    uint32_t outst_pf = seeded && cfg.hunger_init_full ? cfg.nwaves : 0u;
     uint32_t outst_cur = 0, hunger_in = 0;
     // nothing from the set-up stays in flight into the loop: a load whose
     // register the loop's first batch body overwrites would make the

@@ -17,11 +17,11 @@ T = {"T1": ("-t 1 -a 3 -d 10 -b 4 -r 19", 4130071), "T3L": ("-t 0 -b 2000 -q 0.2
      "T3": ("-t 0 -b 2000 -q 0.124875 -m 8 -r 42", 4112897)}
 args, nodes = T[os.environ["HX_TREE"]]
 ms = []
-for _ in range(3):
+for _ in range(int(os.environ.get("HX_REPS", "3"))):
     r = H.uts(args)
     assert r["nodes"] == nodes, r["nodes"]
     ms.append(r["kernel_ms"])
-print(json.dumps(min(ms)))
+print(json.dumps(sorted(ms)))
 '''
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tree, rounds, settings = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
@@ -36,7 +36,9 @@ for r in range(rounds):
         if p.returncode != 0:
             print(p.stderr[-1500:], flush=True)
             sys.exit(1)
-        res[s].append(json.loads(p.stdout.strip().splitlines()[-1]))
-        print(f"round {r} [{s or 'default'}]: {res[s][-1]:.3f} ms", flush=True)
+        res[s] += json.loads(p.stdout.strip().splitlines()[-1])
+        print(f"round {r} [{s or 'default'}]: {min(res[s]):.3f} ms best so far", flush=True)
 for s in settings:
-    print(f"{tree} [{s or 'default'}] best {min(res[s]):.3f} ms", flush=True)
+    v = sorted(res[s])
+    print(f"{tree} [{s or 'default'}] best {v[0]:.4f} median {v[len(v) // 2]:.4f} mean {sum(v) / len(v):.4f} ms "
+          f"({len(v)} launches)", flush=True)
