@@ -269,21 +269,16 @@ def load_pmc_traffic():
 
 def load_triad_ceiling():
     """The measured HBM ceiling of the triad's 2-read / 1-write mix
-    (scripts/ubench/ub_triad_ceiling.hip -> profiles/r06/triad_ceiling.jsonl:
+    (scripts/ubench/ub_triad_ceiling.hip -> profiles/r06/triad_ceiling.json:
     13 kernel forms x 5 occupancies, register and LDS-DMA loads, nt and
     default policies). Returns the best average rate of
     any triad form, the form, and the read-only / write-only ceilings of the
     same run, or None."""
-    p = os.path.join(ROOT, "profiles", "r06", "triad_ceiling.jsonl")
-    rows = []
+    p = os.path.join(ROOT, "profiles", "r06", "triad_ceiling.json")
     try:
         with open(p) as f:
-            for line in f:
-                try:
-                    rows.append(json.loads(line))
-                except ValueError:
-                    pass
-    except OSError:
+            rows = json.load(f)["rows"]
+    except (OSError, ValueError, KeyError):
         return None
     tri = [r for r in rows if r["form"].startswith("triad")]
     if not tri:
@@ -293,7 +288,7 @@ def load_triad_ceiling():
     wr = max((r["gbs_avg"] for r in rows if r["form"].startswith("write1")), default=None)
     return {"gbs": best["gbs_avg"], "form": f"{best['form']}, {best['wg_per_cu']} WG/CU", "read2_gbs": rd,
             "write1_gbs": wr, "forms_measured": len(tri),
-            "source": "profiles/r06/triad_ceiling.jsonl (scripts/ubench/ub_triad_ceiling.hip, 2^28 fp32, "
+            "source": "profiles/r06/triad_ceiling.json (scripts/ubench/ub_triad_ceiling.hip, 2^28 fp32, "
                       "hipEvents over 20 launches, same allocation layout as here)"}
 
 
