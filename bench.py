@@ -826,7 +826,7 @@ def main():
         out["configs"] = {
             # roofline_frac: T1 against the same SHA-1 issue ceiling as
             # roofline_uts (a 4.1 M-node tree: its launch ramp and drain show
-            # here, DESIGN.md §10)
+            # here, DESIGN.md §7)
             "uts_t1_1gpu": {"nodes_per_s": t1_rate, "kernel_ms": t1["kernel_ms"],
                             "roofline_frac": t1_rate / out["roofline_uts"]["peak"] if "roofline_uts" in out else None},
             "forasync_triad_2p28": {"GB_per_s": tri["gbs"], "ms": tri["ms"]},

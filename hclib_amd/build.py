@@ -35,16 +35,19 @@ CFLAGS = [
 ]
 
 
-VARIANTS = {"stamps": ["-DHX_STAMPS=1"], "trace": ["-DHX_TRACE=1"], "timeline": ["-DHX_TIMELINE=1"],
-            "strict": ["-DHX_STRICT_HANDOFF=1"],
-            "narrow_noinline": ["-DHX_NARROW_NOINLINE=1"], "carry_perm": ["-DHX_CARRY_LDS=0"], "base": [], "nohoist": ["-DHX_CARRY_HOIST=0"], "fib_small": ["-DHX_FIB_CAP=512", "-DHX_FIB_SCOPES=256", "-DHX_FIB_PIECES=2"],
-            "sched_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
-            "sched_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
-            # GEO 512-ring piece counts (uts.hip uts_pieces): fixed-shape trees at 5, rule tables at 1
-            "fixed_pieces5": ["-DHX_UTS_FIXED_PIECES_512=5"], "rules_pieces1": ["-DHX_UTS_PIECES_512=1"],
-            "residual_whole": ["-DHX_RESIDUAL_WHOLE=1"], "seedfence1": ["-DHX_SEED_FENCES=1"], "shardloop": ["-DHX_UTS_SHARD_FILTER_IN_LOOP=1"], "nonap": ["-DHX_INBOX_NAP=0"], "spill1": ["-DHX_SPILL_X4=0"], "noafter": ["-DHX_AFTER_BODY=0"], "noasmst": ["-DHX_ASM_HANDOFF_STORES=0"], "nodrain": ["-DHX_DRAIN_BEFORE_LOOP=0"], "phases": ["-DHX_PHASES=1"],
-            "split3": ["-DHX_RESIDUAL_SPLIT_MIN=3"], "split4": ["-DHX_RESIDUAL_SPLIT_MIN=4"],
-            "split8": ["-DHX_RESIDUAL_SPLIT_MIN=8"]}
+VARIANTS = {
+    # diagnostic builds (never benchmarked): per-phase cycle stamps, the SW
+    # DAG's critical-path trace, worker timelines, main-loop batch phases
+    "stamps": ["-DHX_STAMPS=1"], "trace": ["-DHX_TRACE=1"], "timeline": ["-DHX_TIMELINE=1"],
+    "phases": ["-DHX_PHASES=1"],
+    # memory-model alternatives: the formal agent release/acquire fences
+    # around every hand-off (chunks; the seeding's levels), measured slower
+    "strict": ["-DHX_STRICT_HANDOFF=1"], "seedfence1": ["-DHX_SEED_FENCES=1"],
+    # compiler machine-scheduler strategies (within noise on T3L)
+    "sched_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
+    "sched_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+    "base": [],
+}
 
 
 def _hash(paths, cflags):

@@ -31,10 +31,9 @@ struct FibCtx {
 };
 
 // the wave's LDS finish scopes (file scope: every access is a ds_* op)
-#ifndef HX_FIB_SCOPES
-#define HX_FIB_SCOPES 512
-#endif
-constexpr int kFibLocalScopes = HX_FIB_SCOPES;
+// (smaller rings and scope sets at more waves per CU measured slower:
+// 0.83-1.1 vs 0.74 ms, profiles/r04/fibsmall_sweep.log)
+constexpr int kFibLocalScopes = 512;
 __shared__ LocalScopes<kFibLocalScopes> s_fib_scopes;
 // the wave's block of HBM scope ids (hx_finish.h finish_open `blk`)
 __shared__ uint32_t s_fib_blk[2];
@@ -49,9 +48,6 @@ struct FibKind {
     static constexpr int kWords = 4;
     static constexpr bool kPure = false;           // scopes are opened / checked out in HBM
     static constexpr bool kBoundedChildren = true;  // 0 or 2
-#ifdef HX_FIB_PIECES
-    static constexpr int kPieces = HX_FIB_PIECES;  // (small-ring builds: a lane's batch output bound)
-#endif
     using Ctx = FibCtx;
     struct Acc {
         unsigned long long tasks = 0, joins = 0;
@@ -111,7 +107,7 @@ struct FibKind {
         // a leaf returns n: it checks out, and the last task out of each scope
         // runs its continuation inline, up the chain (an unbounded climb:
         // round 4 measured bounded climbs and one level per continuation item
-        // no faster, DESIGN.md §11)
+        // no faster, DESIGN.md Appendix A)
         stamp(-1, tst);
 #if defined(HX_STAMPS) && HX_STAMPS
         uint32_t steps = 0;
@@ -238,10 +234,7 @@ struct FibKind {
     }
 };
 
-#ifndef HX_FIB_CAP
-#define HX_FIB_CAP 1024
-#endif
-constexpr int kFibCap = HX_FIB_CAP;  // ring items per wave (16 KiB of LDS at 1,024)
+constexpr int kFibCap = 1024;  // ring items per wave (16 KiB of LDS)
 
 __global__ __launch_bounds__(64) void k_fib(FibCtx ctx, PoolView pool, SchedGlobals *g,
                                             SchedConfig cfg) {

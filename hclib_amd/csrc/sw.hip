@@ -1850,7 +1850,7 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
     // the promise DAG's 256-row tiles at most 512 wide: the packed-half body,
     // tagged outputs (HCLIB_HIP_SW_PK=0: the band forms)
     // (a two-sweep-wave body was exact but slower, 7.95 vs 6.56 ms, and was
-    // removed in round 5: DESIGN.md §11)
+    // removed in round 5: DESIGN.md Appendix A)
     const bool pk = dag && th == kSwPkTh && tw <= kSwPkMaxTw && env_int("HCLIB_HIP_SW_PK", 1) != 0;
     const size_t nt = ntw * nth;
     const size_t b_s1 = ntw * tw, b_s2 = nth * th;

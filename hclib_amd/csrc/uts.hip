@@ -152,15 +152,9 @@ __device__ __forceinline__ int uts_nc(const UtsCtx &c, int d, uint32_t r, uint32
 // one-iteration push loop, T1XL 49.7 -> 37.6 ms, T1L 4.48 -> 4.04, against
 // 5 pieces (45.0 / 4.17 at 3, 42.3 / 4.43 at 2); rule-table trees keep 5
 // (T4 0.88 -> 2.35 ms at 1, T2 1.37 -> 1.65): profiles/r02/pieces_ab.log
-#ifndef HX_UTS_PIECES_512
-#define HX_UTS_PIECES_512 5
-#endif
-#ifndef HX_UTS_FIXED_PIECES_512
-#define HX_UTS_FIXED_PIECES_512 1
-#endif
 template <int MODE, int CAP>
 constexpr int uts_pieces() {
-    return CAP >= 1024 ? 8 : (CAP >= 512 ? (MODE == kUtsGeoFixed ? HX_UTS_FIXED_PIECES_512 : HX_UTS_PIECES_512) : 1);
+    return CAP >= 1024 ? 8 : (CAP >= 512 ? (MODE == kUtsGeoFixed ? 1 : 5) : 1);
 }
 
 // FEAT = 0: plain search; 1: sharded (nshards > 1) and/or per-level histogram;
@@ -686,9 +680,6 @@ extern "C" int hclib_hip_uts_bucket_check(const hclib_hip_uts_params_t *params, 
     return bad;
 }
 
-#ifndef HX_UTS_SHARD_FILTER_IN_LOOP
-#define HX_UTS_SHARD_FILTER_IN_LOOP 0
-#endif
 static thread_local hclib_hip_uts_launch_t g_last_launch{-1, 0, 0, 0, 0, 0, 0, 0, 0};
 
 extern "C" int hclib_hip_uts_last_launch(hclib_hip_uts_launch_t *out) {
@@ -967,8 +958,7 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
     // fixed-shape shard with split < the seeding's level bound) filters its
     // shard inside the seeding (UtsKind::seed_process) and then runs the
     // plain kernel; otherwise the worker loop itself filters (FEAT = 1)
-    // (HX_UTS_SHARD_FILTER_IN_LOOP=1 builds the round-4 form for an A/B)
-    const bool seed_past_split = !HX_UTS_SHARD_FILTER_IN_LOOP && seed.target && nshards > 1 &&
+    const bool seed_past_split = seed.target && nshards > 1 &&
                                  seed.min_levels == (uint32_t)split_depth;
     const bool feat = max_levels > 0 || (nshards > 1 && (global || !seed_past_split));
     if (bin) ctx.bin_thr = (uint32_t)T.rules[1].y;

@@ -115,15 +115,8 @@ __device__ __forceinline__ void ld_sc1_x4x2(const void *p, uint4 &a, uint4 &b) {
 // otherwise wait (vmcnt(0)) for it before the next write to its data
 // register — and so for every load issued since (the scheduler's hand-off
 // words: the loop's next batch body overwrites those registers at once)
-#ifndef HX_ASM_HANDOFF_STORES
-#define HX_ASM_HANDOFF_STORES 1
-#endif
 __device__ __forceinline__ void st_sc1_u32(uint32_t *p, uint32_t v) {
-#if HX_ASM_HANDOFF_STORES
     asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-#else
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 }
 
 // s_waitcnt vmcnt(0) the compiler's waitcnt pass can see (an inline-asm wait

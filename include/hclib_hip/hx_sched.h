@@ -302,15 +302,11 @@ struct SchedConfig {
 // kind with wide nodes can trade residual splitting for LDS, i.e. for more
 // resident waves per CU.
 // A popped range item's residual (children k+1..kend-1) goes back as two
-// halves (default: a wide node's children spread over more batches sooner)
-// or, with HX_RESIDUAL_WHOLE=1 (a measured alternative), as one item
-#ifndef HX_RESIDUAL_WHOLE
-#define HX_RESIDUAL_WHOLE 0
-#endif
-// (a residual shorter than HX_RESIDUAL_SPLIT_MIN children stays whole)
-#ifndef HX_RESIDUAL_SPLIT_MIN
-#define HX_RESIDUAL_SPLIT_MIN 2
-#endif
+// halves, a wide node's children spread over more batches sooner (as one
+// whole item: T1XL 37.4 -> 39.2 ms, profiles/r02/residual_ab.log); a residual
+// of one child stays whole (keeping 3-4 whole was even, 8 slower:
+// residual_split_ab.log)
+constexpr uint32_t kResidualSplitMin = 2;
 
 // a Kind's seeding slots run Kind::seed_process when it has one (UTS: the
 // shard filter at the split depth, which the seeding passes), else process
@@ -364,14 +360,9 @@ struct KindFixedChildren<K, decltype((void)K::kFixedChildren)> {
 };
 constexpr uint32_t kMaxChildren = 1u << 24;  // kend shares its descriptor word with delta
 
-// register carry through LDS (carry_lds) where the ring's stack has room;
-// HX_CARRY_LDS=0 builds keep carry_permute everywhere
-#ifndef HX_CARRY_LDS
-#define HX_CARRY_LDS 1
-#endif
-#ifndef HX_CARRY_HOIST
-#define HX_CARRY_HOIST 1  // the narrow loop's carry slots precomputed (narrow_loop r_fix)
-#endif
+// register carry through LDS (carry_lds) where the ring's stack has room,
+// carry_permute elsewhere (through LDS: T3L 31.29 -> 30.59 ms,
+// profiles/r04/carry_ab_t3l.log)
 template <class Kind, int CAP>
 struct WaveStack {
     static constexpr int TW = Kind::kTmplWords;
@@ -389,7 +380,7 @@ struct WaveStack {
     // register carry's template slots (carry_lds: 2 x 16 B per spawning
     // rank), on the 1,024-item rings only: the 512-item rings of the wide GEO
     // trees run 8 waves per CU, whose stacks then just fit the 160 KiB
-    static constexpr bool kCarryLds = HX_CARRY_LDS && CAP >= 1024;
+    static constexpr bool kCarryLds = CAP >= 1024;
     uint4 cscr[kCarryLds ? 128 : 1];
 };
 
@@ -485,23 +476,19 @@ __device__ __forceinline__ uint32_t *slot_ctl(const PoolView &pool, uint32_t slo
 // producer publishes it after its next batch's body, when the payload stores
 // have long landed (the drain is free there) instead of waiting a round trip
 // for them while it holds the rest of its items.
-#ifndef HX_SPILL_X4
-#define HX_SPILL_X4 1  // chunk payloads as 16-byte sc1 stores / loads (enqueue_chunk, dequeue_chunk)
-#endif
 struct PendingChunk {
     uint32_t slot, pos, q;
     bool live;
 };
 
-// A compiler barrier behind a batch body's results: memory operations after
-// it (the deferred publish, its drain) stay after the body's arithmetic,
-// which has no memory operations of its own to order it
+// Where a compiler barrier behind a batch body's results would go (so that
+// the deferred publish and its drain stay after the body's arithmetic). It
+// is empty: from round 5 until round 6 its guard macro was defined only
+// after this function, so every measured build compiled it out, and the
+// active barrier measured no better (profiles/r06/ab_afterbody.log)
 template <int TW>
 __device__ __forceinline__ void after_body(const uint32_t *child) {
-#if HX_AFTER_BODY
-#pragma unroll
-    for (int i = 0; i < TW; ++i) asm volatile("" ::"v"(child[i]) : "memory");
-#endif
+    (void)child;
 }
 
 template <class Kind, int CAP>
@@ -641,7 +628,7 @@ __device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &poo
         kind_export<Kind>(ctx, w, valid, &g->err);
         kind_trace_item<Kind>(ctx, w, valid, 2u, false);
         if (valid) {
-            if constexpr (HX_SPILL_X4 && W % 4 == 0) {
+            if constexpr (W % 4 == 0) {
                 // 16-byte sc1 stores (a dword sc1 store costs ~6x the bytes of
                 // a dwordx4 one), written as inline asm, which the compiler's
                 // waitcnt pass does not see: it would otherwise wait for them
@@ -740,7 +727,7 @@ __device__ uint32_t dequeue_chunk(const typename Kind::Ctx &ctx, const PoolView 
     const uint32_t *src = pool.data + (size_t)slot * pool.chunk * W;
     if ((uint32_t)lane < n) {
         uint32_t w[W];
-        if constexpr (HX_SPILL_X4 && W == 8) {
+        if constexpr (W == 8) {
             uint4 a, b;
             ld_sc1_x4x2(&src[(uint32_t)lane * W], a, b);
             w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y, w[6] = b.z, w[7] = b.w;
@@ -1097,23 +1084,6 @@ struct NarrowState {
 #ifndef HX_PHASES
 #define HX_PHASES 0  // diagnostic: main-loop batch phase stamps (run_worker)
 #endif
-#ifndef HX_AFTER_BODY
-#define HX_AFTER_BODY 1
-#endif
-#ifndef HX_DRAIN_BEFORE_LOOP
-#define HX_DRAIN_BEFORE_LOOP 1
-#endif
-#ifndef HX_INBOX_NAP
-#define HX_INBOX_NAP 1  // idle siblings watch their inbox while backing off (run_worker)
-#endif
-#ifndef HX_NARROW_NOINLINE
-#define HX_NARROW_NOINLINE 0  // measured: inlined 34.1-34.5 ms vs 35.7-36.3 ms on T3L (profiles/r02/narrow_inline_ab.log)
-#endif
-#if HX_NARROW_NOINLINE
-#define HX_NARROW_ATTR __attribute__((noinline))
-#else
-#define HX_NARROW_ATTR __forceinline__
-#endif
 // Optional diagnostic: a Kind's Acc with a `mode` field learns whether its
 // tasks run in the narrow loop (1) or the main loop (0).
 template <class A, class = void>
@@ -1140,7 +1110,7 @@ __device__ __forceinline__ void acc_set_wid(A &a, uint32_t w) {
 }
 
 template <class Kind, int CAP>
-__device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
+__device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop(
     const typename Kind::Ctx &ctx_ref, typename Kind::Acc &acc_ref, uint32_t *err, WaveStack<Kind, CAP> &st,
     NarrowState<Kind::kTmplWords> ns) {
     constexpr int TW = Kind::kTmplWords;
@@ -1161,7 +1131,7 @@ __device__ HX_NARROW_ATTR NarrowState<Kind::kTmplWords> narrow_loop(
         rcp_fix = mu_fix ? rcp16(mu_fix) : 0u;
     }
     // ... and so are each lane's carry source slot and child index
-    const bool hoist = HX_CARRY_HOIST && mu_fix != 0;  // (wave-uniform)
+    const bool hoist = mu_fix != 0;  // (wave-uniform)
     const uint32_t r_fix = hoist ? __umul24(lane, rcp_fix) >> 16 : 0u;
     const uint32_t ck_fix = hoist ? lane - __umul24(r_fix, mu_fix) : 0u;
     while (true) {
@@ -1739,7 +1709,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
     // register the loop's first batch body overwrites would make the
     // compiler wait (vmcnt(0)) there in every batch, and so for the
     // one-batch-late hunger read
-    if (HX_DRAIN_BEFORE_LOOP) vm_drain();
+    vm_drain();
     while (true) {
         // the ring bounds are wave-uniform: pin them to SGPRs (the uniformity
         // analysis cannot see through the loop's exits) so the batch's
@@ -1907,7 +1877,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             // siblings the sleep is cut into 64-clock naps that watch this
             // wave's inbox (an LDS read): a sibling's hand-off is taken within
             // one nap instead of after the sleep and the next deque probe
-            if constexpr (WPG > 1 && HX_INBOX_NAP) {
+            if constexpr (WPG > 1) {
                 const uint32_t naps = (spins < 8 || cfg.backoff <= 1) ? 1u : (spins < 64 || cfg.backoff <= 4) ? 3u : 8u;
                 for (uint32_t i = 0; i < naps; ++i) {
                     __builtin_amdgcn_s_sleep(1);
@@ -2008,8 +1978,8 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
                 publish_pending<Kind, CAP>(pool, g, pend);
                 top -= take2;
                 const uint32_t rA = kendA - kA - 1u, rB = hasB ? kendB - kB - 1u : 0u;
-                const uint32_t nresA = rA == 0 ? 0u : (rA < (uint32_t)HX_RESIDUAL_SPLIT_MIN || HX_RESIDUAL_WHOLE ? 1u : 2u);
-                const uint32_t nresB = rB == 0 ? 0u : (rB < (uint32_t)HX_RESIDUAL_SPLIT_MIN || HX_RESIDUAL_WHOLE ? 1u : 2u);
+                const uint32_t nresA = rA == 0 ? 0u : (rA < kResidualSplitMin ? 1u : 2u);
+                const uint32_t nresB = rB == 0 ? 0u : (rB < kResidualSplitMin ? 1u : 2u);
                 const uint32_t uA = ncA > 0 ? (uint32_t)ncA : 0u, uB = (hasB && ncB > 0) ? (uint32_t)ncB : 0u;
                 const uint32_t nchA = uA > (uint32_t)kPieces ? (uint32_t)kPieces : uA;
                 const uint32_t nchB = uB > (uint32_t)kPieces ? (uint32_t)kPieces : uB;
@@ -2091,7 +2061,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
         top -= take_ring;
         // ---- push: residual range of the item + the new task's children
         const uint32_t rlen = has ? kend - k - 1u : 0u;
-        const uint32_t nres = rlen == 0 ? 0u : (rlen < (uint32_t)HX_RESIDUAL_SPLIT_MIN || HX_RESIDUAL_WHOLE ? 1u : 2u);
+        const uint32_t nres = rlen == 0 ? 0u : (rlen < kResidualSplitMin ? 1u : 2u);
         uint32_t ucnt = cnt > 0 ? (uint32_t)cnt : 0u;
         n_exec += has ? 1u : 0u;
         n_spawn += has ? ucnt : 0u;
