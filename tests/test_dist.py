@@ -262,7 +262,7 @@ def test_stalled_leg_is_reported_and_the_line_still_prints():
 # sees the flag and stops, both agree on a gloo control group and re-measure
 # together over a fresh gloo exchange group; the result is exact and the
 # whole leg ends within seconds (not the group's 60 s timeout).
-def _sw_fallback_worker(rank, world, port, s1, s2, tw, th, q, fail_gloo_too):
+def _sw_fallback_worker(rank, world, port, s1, s2, tw, th, q, fail_gloo_too, fail_step=0):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HCLIB_DIST_TIMEOUT_S": "60"})
     import time
@@ -276,7 +276,7 @@ def _sw_fallback_worker(rank, world, port, s1, s2, tw, th, q, fail_gloo_too):
 
     def make_job(xb, group, abort):
         attempts.append(xb)
-        first = len(attempts) == 1
+        first = len(attempts) == 1 + fail_step  # the primary attempt's step fail_step
 
         def inject():
             if r == 1 and (first or fail_gloo_too):
@@ -286,7 +286,7 @@ def _sw_fallback_worker(rank, world, port, s1, s2, tw, th, q, fail_gloo_too):
 
     want = (__import__("oracle.loader", fromlist=["sw_score"]).sw_score(s1, s2, tw, th), (len(s1) // tw) * (len(s2) // th))
     t0 = time.monotonic()
-    res = dist.sw_exchange(make_job, r, w, "gloo", want, steps=1)
+    res = dist.sw_exchange(make_job, r, w, "gloo", want, steps=1 + fail_step)
     el = time.monotonic() - t0
     q.put((r, res, el, attempts))
     q.close()
@@ -294,8 +294,11 @@ def _sw_fallback_worker(rank, world, port, s1, s2, tw, th, q, fail_gloo_too):
     os._exit(0)  # abandoned transfers of the failed attempt: no orderly shutdown
 
 
-@pytest.mark.parametrize("fail_gloo_too", [False, True])
-def test_sw_exchange_failure_falls_back_on_every_rank(fail_gloo_too):
+@pytest.mark.parametrize("fail_gloo_too,fail_step", [(False, 0), (True, 0), (False, 1)])
+def test_sw_exchange_failure_falls_back_on_every_rank(fail_gloo_too, fail_step):
+    """fail_step 1: rank 1 fails in the second step of the primary attempt,
+    after a first step both ranks completed (round-5 advisor: the ranks must
+    not end up in different collectives on the control group)."""
     import random
 
     rng = random.Random(7)
@@ -305,7 +308,7 @@ def test_sw_exchange_failure_falls_back_on_every_rank(fail_gloo_too):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sw_fallback_worker, args=(r, 2, port, s1, s2, tw, th, q, fail_gloo_too))
+    procs = [ctx.Process(target=_sw_fallback_worker, args=(r, 2, port, s1, s2, tw, th, q, fail_gloo_too, fail_step))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -315,7 +318,8 @@ def test_sw_exchange_failure_falls_back_on_every_rank(fail_gloo_too):
         assert p.exitcode == 0
     for r, out, el, attempts in res:
         assert el < 10.0, (r, el)
-        assert attempts == ["gloo", "gloo"], (r, attempts)  # both ranks re-ran, together
+        # both ranks re-ran, together (one job per step of each attempt made)
+        assert attempts[:1 + fail_step] == ["gloo"] * (1 + fail_step) and len(attempts) >= 2 + fail_step, (r, attempts)
         if fail_gloo_too:
             assert "failed" in out and "injected" in out["failed"], (r, out)
         else:
