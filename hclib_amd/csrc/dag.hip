@@ -184,7 +184,7 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
     HX_HIP(hipGetLastError());
     HX_HIP(hipEventRecord(m.ev1, m.stream));
     uint32_t err = 0;
-    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
     HX_HIP(hipMemcpyAsync(&err, v.err, 4, hipMemcpyDeviceToHost, m.stream));
     HX_HIP(hipMemcpyAsync(st, v.stats, sizeof(st), hipMemcpyDeviceToHost, m.stream));
     std::vector<uint32_t> sat;
@@ -222,8 +222,6 @@ extern "C" int hclib_hip_dag_end(const char *who, uint64_t *datum_out, uint8_t *
         fprintf(stderr, "dag group phases (cycles per task, wave 0): take %.0f body %.0f put %.0f\n",
                 (double)st[3] / st[0], (double)st[4] / st[0], (double)st[5] / st[0]);
 #endif
-    if (getenv("HCLIB_HIP_DAG_SPEC_STATS") && (st[6] | st[7]))
-        fprintf(stderr, "dag speculation: %llu confirmed, %llu refused of %llu tasks\n", st[6], st[7], st[0]);
     if (stats) {
         stats->tasks = st[0];
         stats->puts = st[1];
@@ -362,8 +360,6 @@ extern "C" int hclib_hip_dyn_end(const char *who, hclib_hip_dyn_stats_t *stats) 
     HX_HIP(hipStreamSynchronize(m.stream));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m.ev0, m.ev1);
-    if (getenv("HCLIB_HIP_DAG_SPEC_STATS") && (st[6] | st[7]))
-        fprintf(stderr, "dag speculation: %llu confirmed, %llu refused of %llu tasks\n", st[6], st[7], st[0]);
     if (stats) {
         stats->tasks = st[0];
         stats->puts = st[1];

@@ -1338,41 +1338,16 @@ __host__ __device__ constexpr int sw_pk_lds_words(int tw) {
 }
 inline size_t sw_pk_lds_bytes(int tw) { return (size_t)sw_pk_lds_words(tw) * 4; }
 
-// A speculated tile's decision (hx_dag.h run_dag_group_spec): tag 0 = the
-// tile is not speculative; otherwise the decision word reads tag | 1 once
-// this workgroup's put released the tile, tag | 2 once it did not
-struct SwSpec {
-    const uint32_t *word = nullptr;
-    // (0 once this wave has seen the release: every later check is free — a
-    // poll's extra LDS read per round slowed the sweep beside it ~4 %)
-    mutable uint32_t tag = 0;
-    // the score ring's counters (misc[5] / misc[6]) at this tile's start:
-    // run_dag_group_spec starts the next tile with no barrier between, so
-    // they run on across tiles instead of being reset (0 under run_dag_group)
-    int cb = 0;
-    // 1 go, 2 abort, 0 still pending
-    __device__ __forceinline__ uint32_t state() const {
-        if (!tag) return kSpecGo;
-        const uint32_t v = __builtin_amdgcn_readfirstlane(lds_load(word));
-        const uint32_t st = (v & ~3u) == tag ? (v & 3u) : 0u;
-        if (st == kSpecGo) tag = 0;
-        return st;
-    }
-    __device__ __forceinline__ bool aborted() const { return tag && state() == kSpecAbort; }
-};
-
 // wait until an LDS counter reaches `want` (bounded; device error on timeout)
 // EQ: wait for the flag to equal `want` (a per-tile flag whose tiles are not
 // monotone per workgroup: tile (1, 0) is id ntw and tile (0, 2) may run after
-// it); otherwise for it to reach `want` (counters that only grow). A refused
-// speculation (sp) ends the wait with false.
+// it); otherwise for it to reach `want` (counters that only grow)
 template <bool EQ = false>
-__device__ __forceinline__ bool sw_pk_wait(const SwCtx &c, const int *flag, int want, const SwSpec &sp = SwSpec{}) {
+__device__ __forceinline__ bool sw_pk_wait(const SwCtx &c, const int *flag, int want) {
     auto done = [&]() { return EQ ? lds_flag_ld(flag) == want : lds_flag_ld(flag) >= want; };
     if (done()) return true;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t n = 1; !done(); ++n) {
-        if (sp.aborted()) return false;
         __builtin_amdgcn_s_sleep(1);
         if ((n & 255) == 0) {
             if (ld_agent(c.err)) return false;
@@ -1441,7 +1416,7 @@ __device__ bool sw_pk_stage(const SwCtx &c, int R0, int C0, int ncols, int *sel,
 
 // The score wave: every chunk's scores from the staged selectors and rows.
 __device__ bool sw_pk_scores(const SwCtx &c, int ncols, uint4 *ring, const int *sel, const int *tbl, int *misc,
-                             int k0 = 0, int k1 = 1 << 30, const SwSpec &sp = SwSpec{}) {
+                             int k0 = 0, int k1 = 1 << 30) {
     const int lane = lane_id();
     const int selw = sw_pk_selw(ncols);
     const uint32_t mlo0 = (uint32_t)tbl[lane], mlo1 = (uint32_t)tbl[64 + lane];
@@ -1449,12 +1424,12 @@ __device__ bool sw_pk_scores(const SwCtx &c, int ncols, uint4 *ring, const int *
     const int *selp = sel + (lane & 3) * selw + 64 + (lane & 3) - lane;  // + s: column s - lane, aligned
     const int nch = (ncols + 127 + 63) / 64;
     for (int k = k0; k < nch && k < k1; ++k) {
-        if (k >= kSwPkSlots && !sw_pk_wait(c, &misc[6], sp.cb + k + 1 - kSwPkSlots, sp)) return false;
+        if (k >= kSwPkSlots && !sw_pk_wait(c, &misc[6], k + 1 - kSwPkSlots)) return false;
         uint4 *dst = ring + (size_t)((k % kSwPkSlots) * 32) * 64 + lane;
-        const int *sb = selp + 64 * k;
+        const int *sp = selp + 64 * k;
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-            const int4 sv = *(const int4 *)(sb + 4 * g);
+            const int4 sv = *(const int4 *)(sp + 4 * g);
             dst[(2 * g) * 64] = make_uint4(__builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv.x),
                                            __builtin_amdgcn_perm(mhi1, mlo1, (uint32_t)sv.x),
                                            __builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv.y),
@@ -1464,27 +1439,7 @@ __device__ bool sw_pk_scores(const SwCtx &c, int ncols, uint4 *ring, const int *
                                                __builtin_amdgcn_perm(mhi0, mlo0, (uint32_t)sv.w),
                                                __builtin_amdgcn_perm(mhi1, mlo1, (uint32_t)sv.w));
         }
-        if (k == 1 && sp.tag) {
-            // a speculated tile: the sweep writes the first bottom-row
-            // granules (what other workgroups read) at the end of chunk 1, so
-            // chunk 1 is held until the release is decided — one memory round
-            // trip after the tile started, normally long in; refused, the
-            // sweep (waiting on the chunk) sees it and leaves
-            const unsigned long long td = __builtin_amdgcn_s_memrealtime();
-            uint32_t st;
-            for (uint32_t n = 1; (st = sp.state()) == 0u; ++n) {
-                __builtin_amdgcn_s_sleep(1);
-                if ((n & 255) == 0) {
-                    if (ld_agent(c.err)) return false;
-                    if (__builtin_amdgcn_s_memrealtime() - td > 100000ull * c.spin_ms) {
-                        if (lane == 0) dev_error(c.err, kErrSpinTimeout);
-                        return false;
-                    }
-                }
-            }
-            if (st == kSpecAbort) return false;
-        }
-        if (lane == 0) lds_flag_st(&misc[5], sp.cb + k + 1);
+        if (lane == 0) lds_flag_st(&misc[5], k + 1);
     }
     return true;
 }
@@ -1493,8 +1448,7 @@ __device__ bool sw_pk_scores(const SwCtx &c, int ncols, uint4 *ring, const int *
 // workgroup's top-row array (sw_pk_topw words, 16-byte aligned). KX =
 // columns per lane (ncols <= 64 KX).
 template <int KX>
-__device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const uint4 *ring, int *misc,
-                           const SwSpec &sp = SwSpec{}) {
+__device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const uint4 *ring, int *misc) {
     const int lane = lane_id();
     const int ncols = T.ncols, R0 = T.R0, C0 = T.C0;
     const int topw = sw_pk_topw(ncols);
@@ -1535,7 +1489,6 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
 #pragma unroll
         for (int k = 0; k < KX; ++k) ready = ready && (!T.hin || (th_[k] >> 32) == 1ull);
         if (__ballot(!ready) == 0) break;
-        if (sp.aborted()) return false;  // (a refused speculation: its inputs may never come)
         __builtin_amdgcn_s_sleep(1);
         if ((n & 63) == 63) {
             if (ld_agent(c.err)) return false;
@@ -1616,7 +1569,7 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
     const int nsteps = ncols + 127;
     const int Rb = R0 + kSwPkTh;  // the bottom row's matrix row
     for (int s0 = 0, k = 0; s0 < nsteps; s0 += 64, ++k) {
-        if (!sw_pk_wait(c, &misc[5], sp.cb + k + 1, sp)) return false;
+        if (!sw_pk_wait(c, &misc[5], k + 1)) return false;
         if (k == 0) tstamp(12);  // the first chunk's scores are there
         const uint4 *src = ring + (size_t)((k % kSwPkSlots) * 32) * 64 + lane;
         uint32_t acc = 0;
@@ -1656,7 +1609,7 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
                 lr1 = h1;
             }
         }
-        if (lane == 0) lds_flag_st(&misc[6], sp.cb + k + 1);  // the chunk's ring slot is free
+        if (lane == 0) lds_flag_st(&misc[6], k + 1);  // the chunk's ring slot is free
         // lanes 32 + p hold steps s0 + 2p (low half) and s0 + 2p + 1 (high)
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -1696,7 +1649,7 @@ __device__ bool sw_pk_tile(const SwCtx &c, const SwPkTile &T, int *top, const ui
 // runs (misc + kSwPkMisc + 256, then misc[8] = t + 1), so a kept neighbour
 // starts without a global load. Gives up once this tile is done (misc[4]):
 // the next tile then loads the row itself.
-__device__ __forceinline__ void sw_pk_prefetch_top(const SwCtx &c, uint32_t t, int *misc, const SwSpec &sp) {
+__device__ __forceinline__ void sw_pk_prefetch_top(const SwCtx &c, uint32_t t, int *misc) {
     int *ntop = misc + kSwPkMisc + 256;
     const sw_gran *src = c.gbot + (size_t)(t + 1 - (uint32_t)c.ntw) * c.tw;
     const int xmax = c.tw - 1;
@@ -1719,7 +1672,7 @@ __device__ __forceinline__ void sw_pk_prefetch_top(const SwCtx &c, uint32_t t, i
             if (lane_id() == 0) lds_flag_st(&misc[8], (int)t + 1);
             return;
         }
-        if (lds_flag_ld(&misc[4]) == (int)t + 1 || sp.aborted()) return;
+        if (lds_flag_ld(&misc[4]) == (int)t + 1) return;
         __builtin_amdgcn_s_sleep(8);
     }
 }
@@ -1733,32 +1686,6 @@ struct SwDagPkKind {
     static constexpr bool kSc1Payload = true;  // tile inputs/outputs move by ld_agent / st_agent
     static constexpr bool kTagged = true;      // ... as tagged granules: puts without a drain
     static constexpr bool kReserve = true;     // ready slots taken beside the counter decrements
-    // the right neighbour (the task a tile's put keeps when it releases it)
-    // starts while the put is in flight (hx_dag.h run_dag_group_spec) —
-    // when its top row is already here (misc[8], the up-right tile's bottom
-    // row polled complete while this tile ran; always on the first tile row):
-    // then the put almost always releases it. Otherwise a refused speculation
-    // would hold the workgroup off the ready list for a round trip
-    static constexpr bool kSpeculate = true;
-    static constexpr int kPredictWave = 1;  // the score wave: it wrote misc[8]
-    __device__ static uint32_t predict(const SwCtx &c, uint32_t t) {
-        const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
-        if (j + 1 >= c.ntw) return kDagEmpty;
-        return (i == 0 || misc_of(c)[8] == (int)t + 1) ? t + 1 : kDagEmpty;
-    }
-    __device__ static uint32_t *spec_word(const SwCtx &c) { return (uint32_t *)&misc_of(c)[9]; }
-    // the score ring's chunks per tile (the counters' step, SwSpec::cb)
-    __device__ static int nchunks(const SwCtx &c) { return (c.tw + 127 + 63) / 64; }
-    // between tasks under run_dag_group_spec: the last tile run (its LDS
-    // outputs feed a kept right neighbour); after a refused speculation the
-    // ring counters move to the next task's base (the tile never ran; misc[0]
-    // stays)
-    __device__ static void after_task(const SwCtx &c, uint32_t t) { misc_of(c)[0] = (int)t; }
-    __device__ static void after_abort(const SwCtx &c, uint32_t, uint32_t seq_next) {
-        int *misc = misc_of(c);
-        misc[5] = (int)seq_next * nchunks(c);
-        misc[6] = (int)seq_next * nchunks(c);
-    }
     __device__ static int *misc_of(const SwCtx &c) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
         return sw_lds + sw_pk_lds_words(c.tw) - kSwPkMisc - 256 - kSwPkMaxTw;
@@ -1768,23 +1695,17 @@ struct SwDagPkKind {
     // [5] / [6] score chunks written / read, [7] the tile whose selectors and
     // score rows are staged (misc + 16: the rows, [4][64]), [8] the tile whose
     // top row (H) is in LDS (misc + 16 + 256: the right neighbour's top row,
-    // taken while this tile runs once every granule's tag is set), [9..12]
-    // the speculation's words (run_dag_group_spec)
-    __device__ static bool run_group(const SwCtx &c, uint32_t t, const uint32_t *, int wave, uint32_t spec_tag = 0,
-                                     uint32_t seq = 0) {
+    // taken while this tile runs once every granule's tag is set)
+    __device__ static bool run_group(const SwCtx &c, uint32_t t, const uint32_t *, int wave) {
         extern __shared__ __attribute__((aligned(16))) int sw_lds[];
         int *misc = misc_of(c);
-        SwSpec sp;
-        sp.word = (const uint32_t *)&misc[9];
-        sp.tag = spec_tag;
-        sp.cb = (int)seq * nchunks(c);
         uint4 *ring = (uint4 *)sw_lds;
         int *top = sw_lds + kSwPkRingU4 * 4, *sel = top + sw_pk_topw(c.tw), *right_keep = sel + 4 * sw_pk_selw(c.tw);
         const int i = (int)(t / (uint32_t)c.ntw), j = (int)(t % (uint32_t)c.ntw);
         if (wave == 2) {
             // run_dag_group's helper (the workgroup's last wave): returns once
             // the tile's LDS outputs (the corner datum) exist
-            return sw_pk_wait<true>(c, &misc[4], (int)t + 1, sp);
+            return sw_pk_wait<true>(c, &misc[4], (int)t + 1);
         }
         if (wave == 1) {
             int *tbl = misc + kSwPkMisc;
@@ -1792,12 +1713,12 @@ struct SwDagPkKind {
             // soon as its columns are staged, the rest after
             bool ok = true;
             if (misc[7] != (int)t) {
-                auto first = [&]() { return sw_pk_scores(c, c.tw, ring, sel, tbl, misc, 0, 1, sp); };
+                auto first = [&]() { return sw_pk_scores(c, c.tw, ring, sel, tbl, misc, 0, 1); };
                 ok = c.tw <= 256 ? sw_pk_stage<4>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl, first)
                                  : sw_pk_stage<8>(c, i * kSwPkTh, j * c.tw, c.tw, sel, tbl, first);
-                if (ok) ok = sw_pk_scores(c, c.tw, ring, sel, tbl, misc, 1, 1 << 30, sp);
+                if (ok) ok = sw_pk_scores(c, c.tw, ring, sel, tbl, misc, 1);
             } else {
-                ok = sw_pk_scores(c, c.tw, ring, sel, tbl, misc, 0, 1 << 30, sp);
+                ok = sw_pk_scores(c, c.tw, ring, sel, tbl, misc);
             }
             if (!ok) return false;
             // while the sweep runs: stage the right neighbour
@@ -1813,7 +1734,7 @@ struct SwDagPkKind {
             // starts without a global load
             // (after the sweep wave has read this tile's own LDS top row: it
             // consumes chunk 0 only after that)
-            if (next && i > 0 && sw_pk_wait(c, &misc[6], sp.cb + 1, sp)) sw_pk_prefetch_top(c, t, misc, sp);
+            if (next && i > 0 && sw_pk_wait(c, &misc[6], 1)) sw_pk_prefetch_top(c, t, misc);
             return true;
         }
         const bool from_lds = j > 0 && misc[0] == (int)t - 1;
@@ -1835,7 +1756,7 @@ struct SwDagPkKind {
         T.corner_out_lds = &misc[3];
         T.corner_lds = &misc[1 + (t & 1)];
         T.trec = HX_DAG_TRACE && c.dtrace ? c.dtrace + (size_t)t * kDagTraceWords : nullptr;
-        const bool ok = c.tw <= 256 ? sw_pk_tile<4>(c, T, top, ring, misc, sp) : sw_pk_tile<8>(c, T, top, ring, misc, sp);
+        const bool ok = c.tw <= 256 ? sw_pk_tile<4>(c, T, top, ring, misc) : sw_pk_tile<8>(c, T, top, ring, misc);
         if (ok && lane_id() == 0) lds_flag_st(&misc[4], (int)t + 1);
         return ok;
     }
@@ -1862,9 +1783,6 @@ struct SwDagPkKind {
     }
 };
 
-// SPEC: the right neighbour starts while the put that may release it is in
-// flight (run_dag_group_spec); otherwise run_dag_group
-template <bool SPEC>
 __global__ __launch_bounds__(192) void k_sw_dag_pk(SwCtx c, DagView v) {
     int *misc = SwDagPkKind::misc_of(c);
     if (threadIdx.x == 0) {
@@ -1874,10 +1792,8 @@ __global__ __launch_bounds__(192) void k_sw_dag_pk(SwCtx c, DagView v) {
         misc[6] = 0;
         misc[7] = -1;  // no tile's scores staged
         misc[8] = -1;  // no tile's top row in LDS
-        misc[9] = 0;   // no speculation decided ([9..12]: run_dag_group_spec's words)
     }
-    if constexpr (SPEC) run_dag_group_spec<SwDagPkKind>(c, v);
-    else run_dag_group<SwDagPkKind>(c, v, nullptr);
+    run_dag_group<SwDagPkKind>(c, v, nullptr);
 }
 
 __global__ void k_sw_init(uint32_t *deps, uint32_t *ready, int ntw, int nth) {
@@ -2041,11 +1957,9 @@ extern "C" int hclib_hip_sw(const int8_t *s1, size_t n1, const int8_t *s2, size_
         if (pk) {
             const size_t plds = sw_pk_lds_bytes(tw);
             c.dtrace = ((const DagView *)L.view)->trace;
-            const bool spec = env_int("HCLIB_HIP_SW_SPEC", 0) != 0;
-            const void *kp = spec ? (const void *)k_sw_dag_pk<true> : (const void *)k_sw_dag_pk<false>;
-            if (plds > 64 * 1024) (void)hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
-            if (spec) hipLaunchKernelGGL(k_sw_dag_pk<true>, dim3(L.grid), dim3(192), plds, m.stream, c, *(const DagView *)L.view);
-            else hipLaunchKernelGGL(k_sw_dag_pk<false>, dim3(L.grid), dim3(192), plds, m.stream, c, *(const DagView *)L.view);
+            if (plds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_pk,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
+            hipLaunchKernelGGL(k_sw_dag_pk, dim3(L.grid), dim3(192), plds, m.stream, c, *(const DagView *)L.view);
         } else if (wg) {
             const size_t blds = sw_band_lds_bytes(th / bh) + (4 + 2 * (size_t)th) * 4;  // + kept right columns
             if (blds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k_sw_dag_wg,

@@ -754,260 +754,4 @@ __device__ void run_dag_group(const typename Kind::Ctx &ctx, const DagView &view
     }
 }
 
-// Optional: static constexpr bool kSpeculate = true — the workgroup starts
-// the task its put will most likely keep while the put is still in flight
-// (run_dag_group_spec). The Kind then also provides
-//   static constexpr int kPredictWave;                  // the wave that predicts
-//   static uint32_t predict(const Ctx&, uint32_t t);    // that task, or kDagEmpty:
-//        called by kPredictWave at the end of t's body, before the barrier
-//   static uint32_t *spec_word(const Ctx&);             // four LDS words: the
-//        decision, and the kept task / refusal / prediction this function
-//        passes between its waves (in the Kind's own LDS: extra static LDS
-//        here would move the Kind's dynamic LDS base, and with it the bank
-//        mapping its hot loop was tuned for)
-//   static bool run_group(const Ctx&, uint32_t t, const uint32_t *payload,
-//                         int wave, uint32_t spec_tag, uint32_t seq);
-//        seq: this workgroup's task sequence number (0, 1, ...), uniform
-//   static void after_task(const Ctx&, uint32_t t);     // thread 0, after the barrier
-//   static void after_abort(const Ctx&, uint32_t t, uint32_t seq);  // likewise
-// No barrier separates a task's end from the next (speculated) body: what the
-// next body reads of the last one's LDS state must be in place before the
-// barrier that ends it, or written by the wave that reads it.
-// A body run with spec_tag != 0 must not write anything another workgroup
-// reads (nor put) before the decision is in: spec_word == spec_tag | 1 (the
-// put released the task: run it to the end) or spec_tag | 2 (it did not: leave
-// the body, returning false). The decision takes one memory round trip (the
-// counter decrements), far less than a tile's sweep, so the body rarely waits.
-template <class K, class = void>
-struct group_spec { static constexpr bool value = false; };
-template <class K>
-struct group_spec<K, decltype((void)K::kSpeculate)> { static constexpr bool value = K::kSpeculate; };
-constexpr uint32_t kSpecGo = 1u, kSpecAbort = 2u;
-
-// The workgroup form with speculation (tagged, reserved, split puts only).
-// Per task: the helper (last wave) does the previous task's put — decrements,
-// reserved ready slots, the kept task — while the other waves already run the
-// predicted task; if that put did not release it, every wave leaves the body
-// and the workgroup takes the task the put kept, or a ticket. Without a
-// prediction (the last tile of a row) the put runs first and the next task is
-// chosen as in run_dag_group. Every released task still runs exactly once: a
-// speculated body only goes past its decision point when this workgroup's own
-// decrement released it, which no other workgroup's did.
-template <class Kind>
-__device__ void run_dag_group_spec(const typename Kind::Ctx &ctx, const DagView &view) {
-    constexpr int N = group_put_n<Kind>::value;
-    static_assert(N > 0 && group_reserve<Kind>::value && group_tagged<Kind>::value && Kind::kSc1Payload,
-                  "speculation is built on the tagged, reserved, split put");
-    const uint32_t nslots = view.nslots;
-    __shared__ DagGroupShared sh;
-    uint32_t *spec = Kind::spec_word(ctx);
-    uint32_t &s_next = spec[1];     // the task the last put kept for this workgroup (kDagEmpty: none)
-    uint32_t &s_aborted = spec[2];  // the running speculated task was not released by this workgroup
-    uint32_t &s_pred = spec[3];     // the task the last body's kPredictWave predicted
-    DagWave w{view, 0, 0, kDagEmpty, 0, 0};
-    const int lane = lane_id(), wave = (int)(threadIdx.x >> 6), nwaves = (int)(blockDim.x >> 6);
-    const int helper = nwaves - 1;
-    unsigned long long ran = 0;
-    if (threadIdx.x == 0) {
-        sh.fail = 0;
-        s_next = kDagEmpty;
-        s_aborted = 0;
-        *spec = 0;
-    }
-    __syncthreads();
-    // the put of task pt (helper wave): its waiters are in sh.waiter; the
-    // speculated task st is kept if this put released it, else the first
-    // released task is kept for later (s_next); true when st was released
-    auto put = [&](uint32_t pt, uint32_t st) -> bool {
-        const uint32_t nwait = sh.nwait;
-        if (nwait > 64) {  // (the prefetch holds 64 waiter entries)
-            if (lane == 0) dev_error(view.err, kErrBadTask);
-            return false;
-        }
-        uint32_t base = 0, rt = kDagEmpty;
-        if (lane == 0) base = add_agent(view.tail, nwait);
-        if ((uint32_t)lane < nwait) {
-            const uint32_t c = sh.waiter[lane];
-            if (add_agent(&view.deps[c], (uint32_t)-1) == 1u) rt = c;
-        }
-        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-        const bool fits = base + nwait <= nslots;  // (a promise put twice: no ready write past the list)
-        if (!fits && lane == 0) dev_error(view.err, kErrDoublePut);
-        const unsigned long long m = fits ? __ballot(rt != kDagEmpty) : 0ull;
-        const unsigned long long ms = st != kDagEmpty ? (m & __ballot(rt == st)) : 0ull;
-        int kept_lane = -1;
-        uint32_t nx = kDagEmpty;
-        if (ms) {
-            kept_lane = __builtin_ctzll(ms);
-        } else if (m) {
-            kept_lane = __builtin_ctzll(m);
-            nx = (uint32_t)__builtin_amdgcn_readlane((int)rt, kept_lane);
-        }
-        if (fits && (uint32_t)lane < nwait)
-            st_agent(&view.ready[base + (uint32_t)lane], (rt != kDagEmpty && lane != kept_lane) ? rt : kDagSkip);
-#if HX_DAG_TRACE
-        if (view.trace && rt != kDagEmpty) {
-            view.trace[(size_t)rt * kDagTraceWords + 0] = __builtin_amdgcn_s_memrealtime();
-            view.trace[(size_t)rt * kDagTraceWords + 6] = pt;
-            view.trace[(size_t)rt * kDagTraceWords + 4] = lane == kept_lane ? 1ull : 0ull;
-        }
-        if (view.trace && lane == 0) view.trace[(size_t)pt * kDagTraceWords + 3] = __builtin_amdgcn_s_memrealtime();
-#endif
-        if (lane == 0) s_next = nx;
-        w.puts += N;
-        w.releases += (unsigned long long)__builtin_popcountll(m);
-        return ms != 0ull;
-    };
-    // the waiter lists of task t's promises into sh.waiter (helper wave)
-    auto prefetch = [&](uint32_t t) {
-        uint32_t p[N];
-        Kind::promises(ctx, t, p);
-        uint32_t my_p = 0, b = 0, e = 0;
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-            if (lane == i) my_p = p[i];
-        if (lane < N) {
-            b = view.waiter_off[my_p];
-            e = view.waiter_off[my_p + 1];
-        }
-        uint32_t ub[N], un[N], upre[N], total = 0;
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            ub[i] = (uint32_t)__builtin_amdgcn_readlane((int)b, i);
-            un[i] = (uint32_t)__builtin_amdgcn_readlane((int)e, i) - ub[i];
-            upre[i] = total;
-            total += un[i];
-        }
-        if (total <= 64) {
-            uint32_t idx = 0;
-#pragma unroll
-            for (int i = 0; i < N; ++i)
-                if ((uint32_t)lane >= upre[i] && (uint32_t)lane < upre[i] + un[i]) idx = ub[i] + ((uint32_t)lane - upre[i]);
-            if ((uint32_t)lane < total) sh.waiter[lane] = view.waiters[idx];
-        }
-        if (lane == 0) sh.nwait = total;
-    };
-    // the datums of task t and its promises marked satisfied (counted up: a
-    // double put leaves 2, found by hclib_hip_dag_end)
-    auto publish = [&](uint32_t t) {
-        uint32_t p[N];
-        unsigned long long d[N];
-        Kind::promises(ctx, t, p);
-        Kind::datums(ctx, t, d);
-        uint32_t my_p = 0;
-        unsigned long long my_d = 0;
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-            if (lane == i) {
-                my_p = p[i];
-                my_d = d[i];
-            }
-        if (lane < N) {
-            st_agent(&view.datum[my_p], my_d);
-            __hip_atomic_fetch_add(&view.satisfied[my_p], 1u, __ATOMIC_RELAXED, HX_AGENT);
-        }
-    };
-    uint32_t t = kDagEmpty, prev = kDagEmpty, iter = 0;
-    bool speculative = false;
-    while (true) {
-        ++iter;
-        bool go = true;
-        if (!speculative) {
-            // the previous task's put first, then the next task: the one it
-            // kept, or a ticket (as run_dag_group)
-            if (wave == helper && prev != kDagEmpty) put(prev, kDagEmpty);
-            __syncthreads();  // s_next
-            if (wave == 0) {
-                uint32_t tt = s_next;
-                while (tt == kDagEmpty) {
-                    uint32_t ticket = 0;
-                    if (lane == 0) ticket = add_agent(view.head, 1u);
-                    ticket = (uint32_t)__shfl((int)ticket, 0, 64);
-                    if (ticket >= nslots) break;
-                    uint32_t got = kDagEmpty;
-                    if (lane == 0) {
-                        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                        while ((got = ld_agent(&view.ready[ticket])) == kDagEmpty) {
-                            if (ld_agent(view.err)) break;
-                            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull * view.spin_ms) {
-                                dev_error(view.err, kErrSpinTimeout);
-                                break;
-                            }
-                            __builtin_amdgcn_s_sleep(1);
-                        }
-                    }
-                    got = (uint32_t)__shfl((int)got, 0, 64);
-                    if (got == kDagEmpty) break;
-                    if (got != kDagSkip) tt = got;
-                }
-                if (tt != kDagEmpty && tt >= view.ntasks) {
-                    if (lane == 0) dev_error(view.err, kErrBadTask);
-                    tt = kDagEmpty;
-                }
-                if (lane == 0) {
-                    sh.slot = tt;
-                    s_next = kDagEmpty;
-                }
-            }
-            __syncthreads();
-            t = sh.slot;
-            prev = kDagEmpty;
-            if (t == kDagEmpty) break;
-            if (wave == helper) prefetch(t);
-        } else if (wave == helper) {
-            // t (the predicted task) is already starting on the other waves:
-            // the put of prev decides whether it may run to its end
-            go = put(prev, t);
-            if (lane == 0) {
-                s_aborted = go ? 0u : 1u;  // (before the decision: LDS ops of a wave land in order)
-                lds_store(spec, (iter << 2) | (go ? kSpecGo : kSpecAbort));
-            }
-            if (go) prefetch(t);
-        }
-        prev = kDagEmpty;
-#if HX_DAG_TRACE
-        if (view.trace && threadIdx.x == 0) {
-            unsigned long long *r = view.trace + (size_t)t * kDagTraceWords;
-            r[1] = __builtin_amdgcn_s_memrealtime();
-            r[5] = blockIdx.x;
-        }
-#endif
-        const bool ok = Kind::run_group(ctx, t, view.payload + (size_t)t * view.payload_words, wave,
-                                        speculative ? iter << 2 : 0u, iter - 1u);
-        if (wave == helper && go && sh.nwait <= 64) publish(t);
-        // (read before the barrier: the helper rewrites it in the next body,
-        // which starts right after it; the decision was in before any wave
-        // left a body that ran to its end)
-        const bool aborted = speculative && lds_load(&s_aborted) != 0;
-        // a body that left because its speculation was refused is no failure
-        if (!ok && !aborted) sh.fail = 1u;
-        if (ok && wave == Kind::kPredictWave && lane == 0) s_pred = Kind::predict(ctx, t);
-        __syncthreads();
-        if (sh.fail) break;
-#if HX_DAG_TRACE
-        if (speculative && threadIdx.x == 0) add_agent(&view.stats[aborted ? 7 : 6], 1ull);  // (diagnostic counts)
-#endif
-        if (aborted) {
-            // the put of the task before it is done (it refused this one)
-            if (threadIdx.x == 0) Kind::after_abort(ctx, t, iter);
-            speculative = false;
-        } else {
-            if (threadIdx.x == 0) Kind::after_task(ctx, t);
-#if HX_DAG_TRACE
-            if (view.trace && threadIdx.x == 0) view.trace[(size_t)t * kDagTraceWords + 2] = __builtin_amdgcn_s_memrealtime();
-#endif
-            ++ran;
-            prev = t;  // its put is next
-            const uint32_t p = s_pred;
-            speculative = p != kDagEmpty;
-            if (speculative) t = p;
-        }
-    }
-    if (wave == 0 && lane == 0) add_agent(&view.stats[0], ran);
-    if (wave == helper && lane == 0) {
-        add_agent(&view.stats[1], w.puts);
-        add_agent(&view.stats[2], w.releases);
-    }
-}
-
 }  // namespace hx
