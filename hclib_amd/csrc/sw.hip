@@ -1720,22 +1720,28 @@ struct SwDagPkKind {
             } else {
                 ok = sw_pk_scores(c, c.tw, ring, sel, tbl, misc);
             }
-            if (!ok) return false;
-            // while the sweep runs: stage the right neighbour
-            const bool next = j + 1 < c.ntw;
-            auto none = []() { return true; };
-            if (next) {
-                if (c.tw <= 256) sw_pk_stage<4>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl, none);
-                else sw_pk_stage<8>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl, none);
+            if (ok) {
+                // while the sweep runs: stage the right neighbour
+                const bool next = j + 1 < c.ntw;
+                auto none = []() { return true; };
+                if (next) {
+                    if (c.tw <= 256) sw_pk_stage<4>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl, none);
+                    else sw_pk_stage<8>(c, i * kSwPkTh, (j + 1) * c.tw, c.tw, sel, tbl, none);
+                }
+                if (lane_id() == 0) misc[7] = next ? (int)t + 1 : -1;
+                // ... and its top row (the up-right tile's bottom row), polled
+                // while this tile's sweep runs: kept, the right neighbour then
+                // starts without a global load
+                // (after the sweep wave has read this tile's own LDS top row: it
+                // consumes chunk 0 only after that)
+                if (next && i > 0 && sw_pk_wait(c, &misc[6], 1)) sw_pk_prefetch_top(c, t, misc);
             }
-            if (lane_id() == 0) misc[7] = next ? (int)t + 1 : -1;
-            // ... and its top row (the up-right tile's bottom row), polled
-            // while this tile's sweep runs: kept, the right neighbour then
-            // starts without a global load
-            // (after the sweep wave has read this tile's own LDS top row: it
-            // consumes chunk 0 only after that)
-            if (next && i > 0 && sw_pk_wait(c, &misc[6], 1)) sw_pk_prefetch_top(c, t, misc);
-            return true;
+            // one exit, drained: a load this path might leave in flight
+            // (the staging's, on a failed wait) would otherwise put a
+            // vmcnt(0) where the waves' paths join behind the body, and the
+            // sweep wave would wait there for its own output stores
+            vm_drain();
+            return ok;
         }
         const bool from_lds = j > 0 && misc[0] == (int)t - 1;
         SwPkTile T;
