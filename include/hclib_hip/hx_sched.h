@@ -663,8 +663,9 @@ __device__ bool enqueue_chunk(const typename Kind::Ctx &ctx, const PoolView &poo
 
 // Try to take one chunk from deque q into the (empty) stack. Returns the
 // number of entries taken (0 if the deque looked empty). Round trips: the
-// head/tail read, the head CAS, the {seq, cnt} pair, the payload; the slot
-// is handed back with a store nobody waits for.
+// head/tail read, the head CAS beside the {seq, cnt} pair's read, the
+// payload; the slot is handed back with a store nobody waits for
+// (profiles/r06/ab_seqcas.log: the pair after the CAS cost T3L 0.13 ms).
 // `done` (wave-uniform) receives the header's termination flag.
 // Probe statistics of an idle wave (HX_TIMELINE builds: logged at exit)
 struct ProbeStats {
@@ -679,15 +680,22 @@ __device__ uint32_t dequeue_chunk(const typename Kind::Ctx &ctx, const PoolView 
     QueueHdr *h = &pool.hdr[q];
     uint32_t pos = 0, fin = 0;
     int ok = 0, nonempty = 0;
+    unsigned long long sc0 = 0;  // the claimed slot's {seq, cnt}, read beside the claim
     if (lane == 0) {
         // one claim attempt: a ticket below the tail, taken by CAS on the head
         const unsigned long long hd2 = ld_agent((const unsigned long long *)&h->head);
         const uint32_t hd = (uint32_t)hd2, tl = ld_agent(&h->tail);
         fin = (uint32_t)(hd2 >> 32);
         nonempty = (int)(tl - hd) > 0;
-        if (nonempty && cas_agent(&h->head, hd, hd + 1)) {
-            pos = hd;
-            ok = 1;
+        if (nonempty) {
+            // the slot's pair is read in the same round trip as the CAS: a
+            // value that shows the ticket published was stored after its
+            // payload had landed, whoever wins the claim
+            sc0 = ld_agent((const unsigned long long *)slot_ctl(pool, q * pool.cap + (hd & (pool.cap - 1))));
+            if (cas_agent(&h->head, hd, hd + 1)) {
+                pos = hd;
+                ok = 1;
+            }
         }
     }
     done = lane0(fin);
@@ -704,8 +712,8 @@ __device__ uint32_t dequeue_chunk(const typename Kind::Ctx &ctx, const PoolView 
     if (lane == 0) {
         // the producer holds this ticket and is publishing it (bounded wait)
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (true) {
-            const unsigned long long sc = ld_agent((const unsigned long long *)slot_ctl(pool, slot));
+        for (bool first = true;; first = false) {
+            const unsigned long long sc = first ? sc0 : ld_agent((const unsigned long long *)slot_ctl(pool, slot));
             if ((uint32_t)sc == pos + 1) {
                 cnt = (uint32_t)(sc >> 32);
                 break;
