@@ -24,6 +24,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -280,6 +281,39 @@ def load_triad_ceiling():
             rows = json.load(f)["rows"]
     except (OSError, ValueError, KeyError):
         return None
+    return _ceiling_of(rows, "profiles/r06/triad_ceiling.json (scripts/ubench/ub_triad_ceiling.hip, 2^28 fp32, "
+                             "hipEvents over 20 launches, same allocation layout as here; another box)")
+
+
+def measure_triad_ceiling_live():
+    """The same ceiling measured now, on this GPU: the quick mode of
+    scripts/ubench/ub_triad_ceiling.bin (built by __graft_entry__.build())
+    runs the read-only, write-only and four best triad forms at 1 and 2
+    workgroups per CU in a child process (about 2 s). HBM rates differ by a
+    few percent between boxes of the pool, so the line's frac_of_ceiling
+    compares the kernel with the ceiling of the part it ran on. None if the
+    binary is absent or fails (load_triad_ceiling() is the fallback)."""
+    exe = os.path.join(ROOT, "scripts", "ubench", "ub_triad_ceiling.bin")
+    if not os.access(exe, os.X_OK):
+        return None
+    try:
+        r = subprocess.run([exe, "quick"], capture_output=True, text=True, timeout=120)
+    except (OSError, subprocess.SubprocessError):
+        return None
+    if r.returncode:
+        return None
+    rows = []
+    for line in r.stdout.splitlines():
+        try:
+            rows.append(json.loads(line))
+        except ValueError:
+            continue
+    return _ceiling_of(rows, "live: scripts/ubench/ub_triad_ceiling.bin quick on this GPU (2^28 fp32, hipEvents "
+                             "over 20 launches per form, 1 and 2 WG/CU)")
+
+
+def _ceiling_of(rows, source):
+    rows = [r for r in rows if isinstance(r, dict) and "form" in r and "gbs_avg" in r]
     tri = [r for r in rows if r["form"].startswith("triad")]
     if not tri:
         return None
@@ -287,9 +321,7 @@ def load_triad_ceiling():
     rd = max((r["gbs_avg"] for r in rows if r["form"].startswith("read2")), default=None)
     wr = max((r["gbs_avg"] for r in rows if r["form"].startswith("write1")), default=None)
     return {"gbs": best["gbs_avg"], "form": f"{best['form']}, {best['wg_per_cu']} WG/CU", "read2_gbs": rd,
-            "write1_gbs": wr, "forms_measured": len(tri),
-            "source": "profiles/r06/triad_ceiling.json (scripts/ubench/ub_triad_ceiling.hip, 2^28 fp32, "
-                      "hipEvents over 20 launches, same allocation layout as here)"}
+            "write1_gbs": wr, "forms_measured": len(tri), "source": source}
 
 
 def cpu_model() -> str:
@@ -764,7 +796,7 @@ def main():
             "frac_median_launch": tri["gbs_median"] / HBM_PEAK_GBS,
             "bit_exact": tri["bit_exact"],
         }
-        ceil = load_triad_ceiling()
+        ceil = measure_triad_ceiling_live() or load_triad_ceiling()
         if ceil:
             # what the 2R + 1W mix reaches at best on this part (no kernel
             # form measured faster), beside the 8 TB/s spec peak

@@ -17,6 +17,7 @@
 // product's form software-pipelined (next loads before this store).
 //   hipcc --offload-arch=gfx950 -O3 scripts/ubench/ub_triad_ceiling.hip -o scripts/ubench/ub_triad_ceiling.bin
 #include <hip/hip_runtime.h>
+#include <string>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -184,7 +185,10 @@ void timeit(const char *name, int bpc, double bytes, F f) {
     fflush(stdout);
 }
 
-int main() {
+// `quick` (bench.py's live ceiling): the read-only, write-only and best
+// triad forms of the full sweep at 1 and 2 workgroups per CU only
+int main(int argc, char **argv) {
+    const bool quick = argc > 1 && std::string(argv[1]) == "quick";
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     const int64_t pad = 0x201000 / 4;
@@ -196,6 +200,18 @@ int main() {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     for (int bpc : {1, 2, 3, 4, 8}) {
         const dim3 g(cus * bpc), t(256);
+        if (quick) {
+            if (bpc > 2) break;
+            timeit("read2 U2", bpc, 8.0 * N, [&] { hipLaunchKernelGGL(k_read2<2>, g, t, 0, 0, b, c, o); });
+            timeit("write1 U4", bpc, 4.0 * N, [&] { hipLaunchKernelGGL(k_write1<4>, g, t, 0, 0, a, 3.f); });
+            timeit("triad U1", bpc, 12.0 * N, [&] { hipLaunchKernelGGL((k_triad<1, false>), g, t, 0, 0, a, b, c, 3.f); });
+            timeit("triad U1 pf", bpc, 12.0 * N, [&] { hipLaunchKernelGGL(k_triad_pf, g, t, 0, 0, a, b, c, 3.f); });
+            timeit("triadL D2 nt", bpc, 12.0 * N,
+                   [&] { hipLaunchKernelGGL((k_triad_lds<2, 2>), g, t, 0, 0, a, b, c, 3.f); });
+            timeit("triadL D4 nt", bpc, 12.0 * N,
+                   [&] { hipLaunchKernelGGL((k_triad_lds<4, 2>), g, t, 0, 0, a, b, c, 3.f); });
+            continue;
+        }
         timeit("read2 U2", bpc, 8.0 * N, [&] { hipLaunchKernelGGL(k_read2<2>, g, t, 0, 0, b, c, o); });
         timeit("read2 U4", bpc, 8.0 * N, [&] { hipLaunchKernelGGL(k_read2<4>, g, t, 0, 0, b, c, o); });
         timeit("write1 U4", bpc, 4.0 * N, [&] { hipLaunchKernelGGL(k_write1<4>, g, t, 0, 0, a, 3.f); });
