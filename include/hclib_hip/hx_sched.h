@@ -1390,6 +1390,7 @@ __device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Ac
     // consecutive slots) and, for outputs below kSoloCap, to the LDS level
     // buffer at ring entry `lds_out` (~0u: none). Slots are 32 B {template,
     // k, k + 1}, stored as 16-B sc1 accesses; base / count come from `alloc`
+    uint32_t mtag = 1u << 20;  // run_slots' window marks (above any main-loop tag; cleared below)
     auto run_slots = [&](const uint32_t (&tmpl)[TW], uint32_t k, bool valid, uint32_t *dst, uint32_t lds_out,
                          auto &&alloc) -> bool {
         uint32_t child[TW];
@@ -1409,16 +1410,21 @@ __device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Ac
             if (lane == 0) dev_error(err, kErrStackOverflow);
             return false;
         }
-        for (uint32_t o = (uint32_t)lane; __ballot(o < tot); o += 64) {
+        // the node of output o: the last lane whose first output is <= o —
+        // each spawning lane marks its first output's place in the 64-output
+        // window, a max-scan spreads the marks (one LDS round trip a window,
+        // where a binary search over the lanes took six)
+        int owner = 0;
+        for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
+            ++mtag;
+            if (u && excl >= r0 && excl < r0 + 64u) st.mark[excl - r0] = (mtag << 6) | (uint32_t)lane;
+            const uint32_t mk = st.mark[lane];
+            const int sc = wave_scan_max((mk >> 6) == mtag ? (int)(mk & 63u) : -1);
+            const int prev = owner;
+            owner = (int)lane63(sc >= 0 ? sc : prev);
+            const uint32_t o = r0 + (uint32_t)lane;
             if (o < tot) {
-                // the node of output o: the last lane whose first output is <= o
-                int lo = 0, hi = 63;
-#pragma unroll
-                for (int it = 0; it < 6; ++it) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (st.d[kScr + mid].x <= o) lo = mid;
-                    else hi = mid - 1;
-                }
+                const int lo = sc >= 0 ? sc : prev;
                 const uint32_t j = o - st.d[kScr + lo].x;
                 const uint4 t0 = st.t0[kScr + lo];
                 const uint2 t1 = st.t1[kScr + lo];
@@ -1651,6 +1657,7 @@ __device__ void run_worker(const typename Kind::Ctx &ctx, const PoolView &pool, 
             // tree's top levels (the host set outstanding = every wave)
             seeded = true;
             top = seed_levels<Kind, CAP>(ctx, acc, g, st, gid, cfg.nwaves, cfg.spin_limit, n_exec, n_spawn, nbatch, tl);
+            st.mark[lane] = 0;  // (the seeding's window marks)
             active = true;
             tl.log(kTlBusy, top);
             if (top == 0) {
