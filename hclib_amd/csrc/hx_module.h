@@ -69,6 +69,7 @@ int make_pool(uint32_t nq, uint32_t cap, uint32_t chunk, uint32_t words, PoolVie
 // of `seed_words` u32; outstanding then starts at `workers`
 struct SeedCfg {
     uint32_t target, max_levels, words, min_levels;
+    uint32_t solo_cap = 0;  // hx_sched.h Seed::solo_cap
 };
 int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global = false, uint32_t workers = 0,
                 const SeedCfg *seed = nullptr);

@@ -185,6 +185,7 @@ int reset_sched(const PoolView &pool, uint32_t outstanding_init, bool global, ui
         init.seed.target = seed->target;
         init.seed.max_levels = seed->max_levels;
         init.seed.min_levels = seed->min_levels;
+        init.seed.solo_cap = seed->solo_cap;
         init.outstanding = workers;  // every wave holds a unit until it has its share
     }
     if (global) init.gview = m.gview;

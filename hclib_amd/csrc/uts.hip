@@ -925,6 +925,11 @@ extern "C" int hclib_hip_uts_search(const hclib_hip_uts_params_t *params, int sh
         const int per_wave = env_int("HCLIB_HIP_SEED_PER_WAVE", uts_expected_nodes(*params) >= 3e7 ? 32 : 16);
         seed.target = (uint32_t)(grid * per_wave);
         seed.max_levels = (uint32_t)env_int("HCLIB_HIP_SEED_LEVELS", 20);
+        // wave 0 alone runs the levels of at most 128 slots (its ring's room
+        // is 224): a level of 189 (T1's depth 3) is cheaper on the grid
+        // (T1 median 0.2051-0.2067 -> 0.1976-0.2011 ms over 18 + 40 launches,
+        // T1L 2.490 -> 2.465; profiles/r06/sweep_t1_solo*.log)
+        seed.solo_cap = (uint32_t)env_int("HCLIB_HIP_SEED_SOLO", 128);
         // a shard's share is only known past its split (level d holds the
         // slots of depth d + 1, filtered when they run), so the seeding goes
         // on to the split — where the levels up to it fit the seeding's

@@ -156,6 +156,7 @@ struct alignas(256) SchedGlobals {
         uint32_t target;       // distribute once a level holds at least this many entries
         uint32_t max_levels;   // ... or after this many levels
         uint32_t min_levels;   // ... but not before this many (a sharded search: past its split)
+        uint32_t solo_cap;     // wave 0 runs levels of at most this many slots alone (0: the ring's room)
     } seed;
 };
 constexpr int kSeedMaxLevels = 24;
@@ -1469,7 +1470,8 @@ __device__ uint32_t seed_levels(const typename Kind::Ctx &ctx, typename Kind::Ac
         asm volatile("" ::: "memory");
         uint32_t in = 0, out = kSoloCap;
         bool ok = true;
-        while (ok && !stop(E, d) && E <= kSoloCap) {
+        const uint32_t solo = sd.solo_cap && sd.solo_cap < kSoloCap ? sd.solo_cap : kSoloCap;
+        while (ok && !stop(E, d) && E <= solo) {
             uint32_t cnt = 0;
             auto alloc = [&](uint32_t tot) {
                 const uint32_t b0 = cnt;
