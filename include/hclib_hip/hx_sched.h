@@ -1118,6 +1118,60 @@ __device__ __forceinline__ void acc_set_wid(A &a, uint32_t w) {
     if constexpr (acc_has_wid<A>::value) a.wid = w;
 }
 
+// The narrow loop of a fixed-size family (KindFixedChildren, pure, bounded,
+// LDS carry; BIN trees): every spawning lane has exactly mu children, so a
+// level is process -> ballot -> carry, with the wave's task and child counts
+// kept as two scalar sums (the carry and t2) instead of per-lane adds, and no
+// uniformity branches. The general loop below compiled this case to ~70
+// instructions around the SHA-1 with five taken branches per level.
+template <class Kind, int CAP>
+__device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
+    const typename Kind::Ctx &ctx_ref, typename Kind::Acc &acc_ref, uint32_t *err, WaveStack<Kind, CAP> &st,
+    NarrowState<Kind::kTmplWords> ns, uint32_t mu, uint32_t r_fix, uint32_t ck_fix) {
+    constexpr int TW = Kind::kTmplWords;
+    const typename Kind::Ctx ctx = ctx_ref;
+    typename Kind::Acc acc = acc_ref;
+    acc_set_mode(acc, 1u);
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t carry = lane0(ns.carry), batches = 0, s_exec = 0, s_spawn = 0;
+    while (true) {
+        const bool h = lane < carry;
+        uint32_t ch2[TW];
+        const int c2 = Kind::process(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h);
+        ++batches;
+        s_exec += carry;
+        const bool sp = c2 > 0;
+        const unsigned long long sp2 = __ballot(sp);
+        if (!sp2) {
+            carry = 0;
+            break;
+        }
+        const uint32_t t2 = mu * (uint32_t)__builtin_popcountll(sp2);
+        s_spawn += t2;
+        if (t2 > (uint32_t)kWaveSize) {
+            // more than one batch: onto the empty ring
+            const uint32_t rk2 = (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(sp2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sp2, 0u));
+            push_uniform<Kind, CAP>(st, ns.top, mu * rk2, t2, mu, sp, ch2);
+            ns.top += t2;
+            carry = 0;
+            break;
+        }
+        carry_lds_slot<TW>(st.cscr, sp2, ch2, ns.ctmpl, r_fix);
+        ns.ck = ck_fix;
+        carry = t2;
+    }
+    if (lane == 0) {
+        ns.n_exec += s_exec;
+        ns.n_spawn += s_spawn;
+    }
+    ns.carry = carry;
+    ns.batches = batches;
+    acc_set_mode(acc, 0u);
+    acc_ref = acc;
+    return ns;
+}
+
 template <class Kind, int CAP>
 __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop(
     const typename Kind::Ctx &ctx_ref, typename Kind::Acc &acc_ref, uint32_t *err, WaveStack<Kind, CAP> &st,
@@ -1143,6 +1197,10 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop(
     const bool hoist = mu_fix != 0;  // (wave-uniform)
     const uint32_t r_fix = hoist ? __umul24(lane, rcp_fix) >> 16 : 0u;
     const uint32_t ck_fix = hoist ? lane - __umul24(r_fix, mu_fix) : 0u;
+    if constexpr (KindFixedChildren<Kind>::value && Kind::kPure && Kind::kBoundedChildren &&
+                  WaveStack<Kind, CAP>::kCarryLds) {
+        if (hoist) return narrow_loop_fixed<Kind, CAP>(ctx_ref, acc_ref, err, st, ns, mu_fix, r_fix, ck_fix);
+    }
     while (true) {
         const bool h = lane < carry;
         uint32_t ch2[TW];
