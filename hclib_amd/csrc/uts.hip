@@ -312,6 +312,33 @@ struct UtsKind {
         return nc;
     }
 
+    // the fixed-size narrow loop's form (hx_sched.h narrow_loop_fixed; FEAT 0,
+    // where a node counts iff its lane is valid): finish<0> without the node
+    // and leaf counts, which the loop sums per level as wave-uniform values
+    // (nodes = the carry, leaves = the carry less the spawning lanes)
+    static constexpr bool kBulkCount = FEAT == 0;
+    __device__ static __forceinline__ int process_bulk(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
+                                                       uint32_t *child, uint32_t *err, bool valid) {
+        uint32_t ch[5];
+        rng_spawn_dev(t, k, ch);
+        for (int g = 1; g < c.gran; ++g) rng_spawn_dev(t, k, ch);
+        const int h1 = (int)t[5] + 1;
+        int nc = uts_nc<MODE>(c, valid ? h1 : 1, ch[4] & 0x7fffffffu, err);
+        acc.maxd = (valid && (uint32_t)h1 > acc.maxd) ? (uint32_t)h1 : acc.maxd;
+        if (!valid) nc = 0;
+        for (int i = 0; i < 5; ++i) child[i] = ch[i];
+        child[5] = (uint32_t)h1;
+        return nc;
+    }
+    // (lane 0 holds a wave's bulk counts: at most the tree's nodes, < 2^32
+    // for every published tree)
+    __device__ static void count_bulk(Acc &acc, uint32_t nodes, uint32_t leaves) {
+        if (lane_id() == 0) {
+            acc.nodes += nodes;
+            acc.leaves += leaves;
+        }
+    }
+
     // the breadth-first seeding's slots (hx_sched.h seed_levels) run with the
     // shard filter and the top levels' counting rule whatever FEAT is: a
     // seeded shard's levels reach past its split depth (the host launches

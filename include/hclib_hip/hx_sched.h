@@ -355,6 +355,18 @@ template <class K, class = void>
 struct KindFixedChildren {
     static constexpr bool value = false;
 };
+// Optional with kFixedChildren: static constexpr bool kBulkCount = true, a
+// process_bulk (process without the per-lane task and leaf counts) and
+// count_bulk(acc, tasks, leaves) — the fixed-size narrow loop then keeps
+// those counts as wave-uniform sums and hands them over once at its exit
+template <class K, class = void>
+struct KindBulkCount {
+    static constexpr bool value = false;
+};
+template <class K>
+struct KindBulkCount<K, decltype((void)K::kBulkCount)> {
+    static constexpr bool value = K::kBulkCount;
+};
 template <class K>
 struct KindFixedChildren<K, decltype((void)K::kFixedChildren)> {
     static constexpr bool value = K::kFixedChildren;
@@ -1133,21 +1145,31 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
     typename Kind::Acc acc = acc_ref;
     acc_set_mode(acc, 1u);
     const uint32_t lane = (uint32_t)lane_id();
-    uint32_t carry = lane0(ns.carry), batches = 0, s_exec = 0, s_spawn = 0;
+    constexpr bool kBulk = KindBulkCount<Kind>::value;
+    uint32_t carry = lane0(ns.carry), batches = 0, s_exec = 0, s_spawn = 0, s_leaves = 0;
     while (true) {
         const bool h = lane < carry;
         uint32_t ch2[TW];
-        const int c2 = Kind::process(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h);
+        int c2;
+        if constexpr (kBulk) c2 = Kind::process_bulk(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h);
+        else c2 = Kind::process(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h);
         ++batches;
         s_exec += carry;
         const bool sp = c2 > 0;
         const unsigned long long sp2 = __ballot(sp);
+        const uint32_t nsp = (uint32_t)__builtin_popcountll(sp2);
+        s_leaves += carry - nsp;
         if (!sp2) {
             carry = 0;
             break;
         }
-        const uint32_t t2 = mu * (uint32_t)__builtin_popcountll(sp2);
+        const uint32_t t2 = mu * nsp;
         s_spawn += t2;
+        // the carry runs on every spawning level, also one that does not
+        // carry (its templates are then unused): the LDS reads land straight
+        // in the loop's template registers instead of a copy behind a branch
+        carry_lds_slot<TW>(st.cscr, sp2, ch2, ns.ctmpl, r_fix);
+        ns.ck = ck_fix;
         if (t2 > (uint32_t)kWaveSize) {
             // more than one batch: onto the empty ring
             const uint32_t rk2 = (uint32_t)__builtin_amdgcn_mbcnt_hi(
@@ -1157,10 +1179,9 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
             carry = 0;
             break;
         }
-        carry_lds_slot<TW>(st.cscr, sp2, ch2, ns.ctmpl, r_fix);
-        ns.ck = ck_fix;
         carry = t2;
     }
+    if constexpr (kBulk) Kind::count_bulk(acc, s_exec, s_leaves);
     if (lane == 0) {
         ns.n_exec += s_exec;
         ns.n_spawn += s_spawn;
