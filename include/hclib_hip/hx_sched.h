@@ -1159,7 +1159,8 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
         const unsigned long long sp2 = __ballot(sp);
         const uint32_t nsp = (uint32_t)__builtin_popcountll(sp2);
         s_leaves += carry - nsp;
-        if (!sp2) {
+        // (both exits are off the chain: a chain level spawns and carries)
+        if (__builtin_expect(!sp2, 0)) {
             carry = 0;
             break;
         }
@@ -1170,7 +1171,7 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
         // in the loop's template registers instead of a copy behind a branch
         carry_lds_slot<TW>(st.cscr, sp2, ch2, ns.ctmpl, r_fix);
         ns.ck = ck_fix;
-        if (t2 > (uint32_t)kWaveSize) {
+        if (__builtin_expect(t2 > (uint32_t)kWaveSize, 0)) {
             // more than one batch: onto the empty ring
             const uint32_t rk2 = (uint32_t)__builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(sp2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sp2, 0u));
