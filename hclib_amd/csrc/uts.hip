@@ -316,19 +316,20 @@ struct UtsKind {
     // where a node counts iff its lane is valid): finish<0> without the node
     // and leaf counts, which the loop sums per level as wave-uniform values
     // (nodes = the carry, leaves = the carry less the spawning lanes)
+    // Returns whether the node spawns (its m children; the loop runs only
+    // with m > 0, so the test is the threshold alone)
     static constexpr bool kBulkCount = FEAT == 0;
-    __device__ static __forceinline__ int process_bulk(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
-                                                       uint32_t *child, uint32_t *err, bool valid) {
+    __device__ static __forceinline__ bool process_bulk(const Ctx &c, Acc &acc, const uint32_t *t, uint32_t k,
+                                                        uint32_t *child, uint32_t *err, bool valid) {
+        static_assert(MODE == kUtsBin, "the fixed-size narrow loop runs BIN trees");
         uint32_t ch[5];
         rng_spawn_dev(t, k, ch);
         for (int g = 1; g < c.gran; ++g) rng_spawn_dev(t, k, ch);
         const int h1 = (int)t[5] + 1;
-        int nc = uts_nc<MODE>(c, valid ? h1 : 1, ch[4] & 0x7fffffffu, err);
         acc.maxd = (valid && (uint32_t)h1 > acc.maxd) ? (uint32_t)h1 : acc.maxd;
-        if (!valid) nc = 0;
         for (int i = 0; i < 5; ++i) child[i] = ch[i];
         child[5] = (uint32_t)h1;
-        return nc;
+        return valid && (ch[4] & 0x7fffffffu) < c.bin_thr;
     }
     // (lane 0 holds a wave's bulk counts: at most the tree's nodes, < 2^32
     // for every published tree)

@@ -356,7 +356,9 @@ struct KindFixedChildren {
     static constexpr bool value = false;
 };
 // Optional with kFixedChildren: static constexpr bool kBulkCount = true, a
-// process_bulk (process without the per-lane task and leaf counts) and
+// process_bulk (process without the per-lane task and leaf counts, returning
+// whether the task spawns its fixed_children() children; called only while
+// that count is > 0) and
 // count_bulk(acc, tasks, leaves) — the fixed-size narrow loop then keeps
 // those counts as wave-uniform sums and hands them over once at its exit
 template <class K, class = void>
@@ -940,13 +942,14 @@ __device__ __forceinline__ void carry_permute(unsigned long long spawn, uint32_t
 // dependent ones (ds_permute -> ds_bpermute -> 6 x ds_bpermute): the wave's
 // LDS operations complete in issue order, so the reads see the stores.
 // The store side, and the read of slot r (this lane's source rank).
+// (`mine`: this lane's bit of `spawn`, when the caller has it as a lane mask
+// already — testing the bit again is three VALU instructions per carry)
 template <int TW>
-__device__ __forceinline__ void carry_lds_slot(uint4 *scr, unsigned long long spawn, const uint32_t *child,
+__device__ __forceinline__ void carry_lds_slot(uint4 *scr, unsigned long long spawn, bool mine, const uint32_t *child,
                                                uint32_t *ctmpl, uint32_t r) {
-    const uint32_t lane = (uint32_t)lane_id();
     const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(spawn >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)spawn, 0u));
-    if ((spawn >> lane) & 1ull) {
+    if (mine) {
         if constexpr (TW == 6) {
             scr[2 * rk] = make_uint4(child[0], child[1], child[2], child[3]);
             *(uint2 *)&scr[2 * rk + 1] = make_uint2(child[4], child[5]);
@@ -975,7 +978,7 @@ __device__ __forceinline__ void carry_lds(uint4 *scr, unsigned long long spawn, 
                                           uint32_t *ctmpl, uint32_t &ck, uint32_t rcp = 0) {
     const uint32_t lane = (uint32_t)lane_id();
     const uint32_t r = __umul24(lane, rcp ? rcp : rcp16(mu)) >> 16;  // lane / mu
-    carry_lds_slot<TW>(scr, spawn, child, ctmpl, r);
+    carry_lds_slot<TW>(scr, spawn, ((spawn >> lane) & 1ull) != 0, child, ctmpl, r);
     ck = lane - __umul24(r, mu);
 }
 
@@ -1150,13 +1153,14 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
     while (true) {
         const bool h = lane < carry;
         uint32_t ch2[TW];
-        int c2;
-        if constexpr (kBulk) c2 = Kind::process_bulk(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h);
-        else c2 = Kind::process(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h);
+        bool sp;
+        if constexpr (kBulk) sp = Kind::process_bulk(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h);
+        else sp = Kind::process(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h) > 0;
         ++batches;
         s_exec += carry;
-        const bool sp = c2 > 0;
-        const unsigned long long sp2 = __ballot(sp);
+        // (the builtin on the lane mask itself: __ballot takes an int and
+        // re-tests it, a select and a compare per level)
+        const unsigned long long sp2 = __builtin_amdgcn_ballot_w64(sp);
         const uint32_t nsp = (uint32_t)__builtin_popcountll(sp2);
         s_leaves += carry - nsp;
         // (both exits are off the chain: a chain level spawns and carries)
@@ -1169,7 +1173,7 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
         // the carry runs on every spawning level, also one that does not
         // carry (its templates are then unused): the LDS reads land straight
         // in the loop's template registers instead of a copy behind a branch
-        carry_lds_slot<TW>(st.cscr, sp2, ch2, ns.ctmpl, r_fix);
+        carry_lds_slot<TW>(st.cscr, sp2, sp, ch2, ns.ctmpl, r_fix);
         ns.ck = ck_fix;
         if (__builtin_expect(t2 > (uint32_t)kWaveSize, 0)) {
             // more than one batch: onto the empty ring
@@ -1262,7 +1266,7 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop(
                 // measured slower: T3L 31.8 -> 32.6 ms, profiles/r04/walk_ab.log)
                 if constexpr (WaveStack<Kind, CAP>::kCarryLds) {
                     if (hoist) {
-                        carry_lds_slot<TW>(st.cscr, sp2, ch2, ns.ctmpl, r_fix);
+                        carry_lds_slot<TW>(st.cscr, sp2, ((sp2 >> lane) & 1ull) != 0, ch2, ns.ctmpl, r_fix);
                         ns.ck = ck_fix;
                     } else {
                         carry_lds<TW>(st.cscr, sp2, mu2, ch2, ns.ctmpl, ns.ck, rcp_fix);
