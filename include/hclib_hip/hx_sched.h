@@ -1149,42 +1149,44 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
     acc_set_mode(acc, 1u);
     const uint32_t lane = (uint32_t)lane_id();
     constexpr bool kBulk = KindBulkCount<Kind>::value;
-    uint32_t carry = lane0(ns.carry), batches = 0, s_exec = 0, s_spawn = 0, s_leaves = 0;
-    while (true) {
+    uint32_t carry = lane0(ns.carry), batches = 0, s_exec = 0, s_spawn = 0, s_leaves = 0, t2;
+    // the task index: at entry the main loop's carry_lds left ck = lane % mu
+    // for the same mu (a fixed family's uniform batch), which is ck_fix, so
+    // every level passes ck_fix (no per-level copy of a loop-carried ck)
+    const uint32_t k = ck_fix;
+    uint32_t ch2[TW];
+    bool sp;
+    unsigned long long sp2;
+    // one exit test per level (t2 = 0: nothing spawned; t2 > one batch: onto
+    // the ring below): a chain level spawns and carries and falls through
+    // to the back-edge
+    do {
         const bool h = lane < carry;
-        uint32_t ch2[TW];
-        bool sp;
-        if constexpr (kBulk) sp = Kind::process_bulk(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h);
-        else sp = Kind::process(ctx, acc, ns.ctmpl, ns.ck, ch2, err, h) > 0;
+        if constexpr (kBulk) sp = Kind::process_bulk(ctx, acc, ns.ctmpl, k, ch2, err, h);
+        else sp = Kind::process(ctx, acc, ns.ctmpl, k, ch2, err, h) > 0;
         ++batches;
         s_exec += carry;
         // (the builtin on the lane mask itself: __ballot takes an int and
         // re-tests it, a select and a compare per level)
-        const unsigned long long sp2 = __builtin_amdgcn_ballot_w64(sp);
+        sp2 = __builtin_amdgcn_ballot_w64(sp);
         const uint32_t nsp = (uint32_t)__builtin_popcountll(sp2);
         s_leaves += carry - nsp;
-        // (both exits are off the chain: a chain level spawns and carries)
-        if (__builtin_expect(!sp2, 0)) {
-            carry = 0;
-            break;
-        }
-        const uint32_t t2 = mu * nsp;
+        t2 = mu * nsp;
         s_spawn += t2;
-        // the carry runs on every spawning level, also one that does not
-        // carry (its templates are then unused): the LDS reads land straight
-        // in the loop's template registers instead of a copy behind a branch
+        // the carry runs on every level, also one that does not carry (its
+        // templates are then unused; with no spawner nothing is written):
+        // the LDS reads land straight in the loop's template registers
         carry_lds_slot<TW>(st.cscr, sp2, sp, ch2, ns.ctmpl, r_fix);
-        ns.ck = ck_fix;
-        if (__builtin_expect(t2 > (uint32_t)kWaveSize, 0)) {
-            // more than one batch: onto the empty ring
-            const uint32_t rk2 = (uint32_t)__builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(sp2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sp2, 0u));
-            push_uniform<Kind, CAP>(st, ns.top, mu * rk2, t2, mu, sp, ch2);
-            ns.top += t2;
-            carry = 0;
-            break;
-        }
         carry = t2;
+    } while (t2 - 1u < (uint32_t)kWaveSize);
+    ns.ck = ck_fix;
+    if (t2 != 0) {
+        // more than one batch: onto the empty ring
+        const uint32_t rk2 = (uint32_t)__builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(sp2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sp2, 0u));
+        push_uniform<Kind, CAP>(st, ns.top, mu * rk2, t2, mu, sp, ch2);
+        ns.top += t2;
+        carry = 0;
     }
     if constexpr (kBulk) Kind::count_bulk(acc, s_exec, s_leaves);
     if (lane == 0) {
