@@ -1149,7 +1149,9 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
     acc_set_mode(acc, 1u);
     const uint32_t lane = (uint32_t)lane_id();
     constexpr bool kBulk = KindBulkCount<Kind>::value;
-    uint32_t carry = lane0(ns.carry), batches = 0, s_exec = 0, s_spawn = 0, s_leaves = 0, t2;
+    // per level: the tasks run (the carry) and the spawning lanes, as scalar
+    // sums; spawned = m x spawners, leaves = tasks - spawners
+    uint32_t carry = lane0(ns.carry), batches = 0, s_exec = 0, s_nsp = 0, t2;
     // the task index: at entry the main loop's carry_lds left ck = lane % mu
     // for the same mu (a fixed family's uniform batch), which is ck_fix, so
     // every level passes ck_fix (no per-level copy of a loop-carried ck)
@@ -1170,9 +1172,8 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
         // re-tests it, a select and a compare per level)
         sp2 = __builtin_amdgcn_ballot_w64(sp);
         const uint32_t nsp = (uint32_t)__builtin_popcountll(sp2);
-        s_leaves += carry - nsp;
+        s_nsp += nsp;
         t2 = mu * nsp;
-        s_spawn += t2;
         // the carry runs on every level, also one that does not carry (its
         // templates are then unused; with no spawner nothing is written):
         // the LDS reads land straight in the loop's template registers
@@ -1188,10 +1189,10 @@ __device__ __forceinline__ NarrowState<Kind::kTmplWords> narrow_loop_fixed(
         ns.top += t2;
         carry = 0;
     }
-    if constexpr (kBulk) Kind::count_bulk(acc, s_exec, s_leaves);
+    if constexpr (kBulk) Kind::count_bulk(acc, s_exec, s_exec - s_nsp);
     if (lane == 0) {
         ns.n_exec += s_exec;
-        ns.n_spawn += s_spawn;
+        ns.n_spawn += mu * s_nsp;
     }
     ns.carry = carry;
     ns.batches = batches;
