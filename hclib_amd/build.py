@@ -35,6 +35,12 @@ CFLAGS = [
 ]
 
 
+# per-source additions: the UTS megakernel under the iterative ILP machine
+# scheduler (T3L 27.00-27.12 -> 26.80-26.82 ms, T1 / T1XL even,
+# profiles/r06/ab_sched_nf.log; per-source: 26.85-27.10 -> 26.72-26.95, T3
+# 2.61 -> 2.58, T1XL +0.2 %, ab_ilp.log; the other sources keep the default)
+SOURCE_FLAGS = {"uts.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
+
 VARIANTS = {
     # diagnostic builds (never benchmarked): per-phase cycle stamps, the SW
     # DAG's critical-path trace, worker timelines, main-loop batch phases
@@ -87,7 +93,7 @@ def build(verbose: bool = True, variant: str = "") -> str:
     hdrs = _headers()
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hdrs, out, cflags), srcs))
+        objs = list(ex.map(lambda s: _compile(s, hdrs, out, cflags + SOURCE_FLAGS.get(s, [])), srcs))
     stamp = os.path.join(out, ".stamp")
     key = "|".join(objs)
     if not os.path.exists(lib) or not os.path.exists(stamp) or open(stamp).read() != key:
