@@ -38,7 +38,9 @@ CFLAGS = [
 # per-source additions: the UTS megakernel under the iterative ILP machine
 # scheduler (T3L 27.00-27.12 -> 26.80-26.82 ms, T1 / T1XL even,
 # profiles/r06/ab_sched_nf.log; per-source: 26.85-27.10 -> 26.72-26.95, T3
-# 2.61 -> 2.58, T1XL +0.2 %, ab_ilp.log; the other sources keep the default)
+# 2.61 -> 2.58, T1XL +0.2 %, ab_ilp.log; the other sources keep the default:
+# the SW kernels are slower under it, 6.46 -> 6.90 ms, ab_sched_sw.log, and
+# fib(30) even, 0.380 / 0.380 ms, ab_fibilp.log)
 SOURCE_FLAGS = {"uts.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 
 VARIANTS = {
